@@ -1,0 +1,243 @@
+/*
+ * mf_hip.h -- C ABI of libmf_hip.so, the MI355X (gfx950) implementation of
+ * the SGD latent-factor update loop of SHEEPididoo/matrix-factorization.
+ *
+ * Drop-in boundary.  The reference crosses from Python into native (numba
+ * JIT) code at exactly three functions of
+ * matrix_factorization/kernel_matrix_factorization.py and four of
+ * matrix_factorization/baseline_model.py; each entry point below replaces
+ * one of them (file:line of the reference cited per function).  The
+ * reference passes NumPy arrays that the callee mutates in place; here the
+ * caller passes device pointers (HBM, e.g. torch-ROCm tensor storage) that
+ * the callee mutates in place, plus an explicit hipStream_t.
+ *
+ * Conventions
+ *   - every function returns 0 on success, a MF_ERR_* code otherwise;
+ *     mf_last_error() returns a thread-local message for the last failure;
+ *   - device pointers are caller-owned; no entry point allocates device
+ *     memory except where a workspace size is documented;
+ *   - `dtype` selects the parameter/rating storage type: MF_F32 or MF_F64;
+ *     ids are int32 (internal ids 0..n-1, -1 = unknown where allowed);
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *     all kernels are enqueued asynchronously on it, no host sync unless the
+ *     optional timing output is requested;
+ *   - host-side schedulers (mf_sched_*) take host pointers and never touch
+ *     the GPU.
+ */
+#ifndef MF_HIP_H
+#define MF_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MF_ABI_VERSION 1
+
+enum {
+    MF_OK = 0,
+    MF_ERR_INVALID = 1,   /* bad argument (shape, enum, range)             */
+    MF_ERR_HIP = 2,       /* HIP runtime error                             */
+    MF_ERR_CAPACITY = 3,  /* caller-provided output buffer too small        */
+    MF_ERR_NOMEM = 4      /* host allocation failed (schedulers)            */
+};
+
+enum { MF_F32 = 0, MF_F64 = 1 };
+
+/* kernel codes: KernelMF(kernel=...) kernel_matrix_factorization.py:56,66 */
+enum { MF_LINEAR = 0, MF_SIGMOID = 1, MF_RBF = 2 };
+
+/* flags for mf_sgd_epoch */
+enum {
+    MF_FLAG_XCD_SWIZZLE = 1   /* map consecutive tiles of a batch onto one XCD */
+};
+
+const char* mf_last_error(void);
+int mf_abi_version(void);
+/* Largest n_factors the kernels accept (inclusive). */
+int mf_max_factors(void);
+
+/*
+ * One SGD epoch over a conflict-free batch schedule.
+ *
+ * Replaces the body of one epoch of `_sgd`
+ * (kernel_matrix_factorization.py:369-425: the sweep that calls
+ * kernel_{linear,sigmoid,rbf}_sgd_update, kernels.py:108-327, once per
+ * rating).  The reference visits ratings in one sequential order.  Here that
+ * order is given as batches: batch b holds the ratings at schedule positions
+ * [batch_offsets[b], batch_offsets[b+1]); no two ratings of a batch share a
+ * user row (when update_user_params) or an item row (when
+ * update_item_params), so every batch is applied in parallel and the result
+ * equals the sequential sweep in the order
+ *     batch_seq[0], batch_seq[1], ...   (each batch in any internal order).
+ * The schedulers below produce such batches (exactly for a given
+ * permutation, or by edge colouring for throughput).
+ *
+ *   user_ids, item_ids, ratings  device, n_ratings each (ratings: dtype)
+ *   order          device, nullable: schedule position -> rating index; when
+ *                  NULL, position p is rating p (ratings pre-sorted)
+ *   batch_offsets  HOST, n_batches + 1 positions (non-decreasing, last <= n)
+ *   batch_seq      HOST, nullable, n_batches: launch order (permutation);
+ *                  NULL = 0, 1, ..., n_batches - 1
+ *   user_biases / item_biases      device, dtype, n_users / n_items
+ *   user_features / item_features  device, dtype, row-major
+ *                  (n_users, n_factors) / (n_items, n_factors)
+ *   kernel, gamma, lr, reg, min_rating, max_rating
+ *                  as KernelMF (a = min_rating, c = max_rating - min_rating,
+ *                  kernel_matrix_factorization.py:405-406)
+ *   update_user_params / update_item_params   as _sgd (:336-337)
+ *   kernel_ms      host, nullable: when given, each batch launch is
+ *                  bracketed by hipEvents, the stream is synchronised and the
+ *                  summed kernel time (ms) is written here.
+ */
+int mf_sgd_epoch(const int32_t* user_ids, const int32_t* item_ids,
+                 const void* ratings, int64_t n_ratings, const int32_t* order,
+                 const int64_t* batch_offsets, const int32_t* batch_seq,
+                 int32_t n_batches, double global_mean, void* user_biases,
+                 void* item_biases, void* user_features, void* item_features,
+                 int32_t n_users, int32_t n_items, int32_t n_factors,
+                 int32_t kernel, int32_t dtype, double gamma, double lr,
+                 double reg, double min_rating, double max_rating,
+                 int32_t update_user_params, int32_t update_item_params,
+                 int32_t flags, void* stream, double* kernel_ms);
+
+/*
+ * Sum of squared training errors, sum_j (r_j - pred_j)^2, accumulated in
+ * FP64 -- replaces `_calculate_rmse` (kernel_matrix_factorization.py:240-317;
+ * rmse = sqrt(sse / n_ratings), :315).  The sum is written to the DEVICE
+ * double *sse_out (no host sync).  `workspace` is a device buffer of at
+ * least mf_sse_workspace_bytes(n_ratings) bytes.  Deterministic: the same
+ * inputs give the same bits.
+ */
+size_t mf_sse_workspace_bytes(int64_t n_ratings);
+int mf_sse(const int32_t* user_ids, const int32_t* item_ids,
+           const void* ratings, int64_t n_ratings, double global_mean,
+           const void* user_biases, const void* item_biases,
+           const void* user_features, const void* item_features,
+           int32_t n_factors, int32_t kernel, int32_t dtype, double gamma,
+           double min_rating, double max_rating, void* workspace,
+           double* sse_out, void* stream);
+
+/*
+ * Predictions for (user, item) pairs -- replaces `_predict`
+ * (kernel_matrix_factorization.py:448-541).  An id of -1 is unknown: zero
+ * bias and an all-zero factor vector (:487-499).  Clipped to
+ * [min_rating, max_rating] when bound_ratings (:532-536).  `out` is a device
+ * array of n_pairs values of `dtype`.
+ */
+int mf_predict(const int32_t* user_ids, const int32_t* item_ids,
+               int64_t n_pairs, double global_mean, const void* user_biases,
+               const void* item_biases, const void* user_features,
+               const void* item_features, int32_t n_factors, int32_t kernel,
+               int32_t dtype, double gamma, double min_rating,
+               double max_rating, int32_t bound_ratings, void* out,
+               void* stream);
+
+/*
+ * Top-`amount` items for each of n_query users (scores = unbounded
+ * prediction of every item, as recommend() scores them,
+ * recommender_base.py:245-260).  Items flagged in the optional device mask
+ * exclude[q * n_items + i] != 0 are skipped.  Ties are broken by the lower
+ * item id.  out_items (int32) / out_scores (dtype): device, n_query * amount.
+ * Rows with fewer than `amount` candidates are padded with id -1.
+ * workspace: device, >= mf_topk_workspace_bytes(n_query, n_items, amount).
+ */
+size_t mf_topk_workspace_bytes(int32_t n_query, int32_t n_items,
+                               int32_t amount);
+int mf_topk(const int32_t* query_users, int32_t n_query, double global_mean,
+            const void* user_biases, const void* item_biases,
+            const void* user_features, const void* item_features,
+            int32_t n_items, int32_t n_factors, int32_t kernel, int32_t dtype,
+            double gamma, double min_rating, double max_rating,
+            const uint8_t* exclude, int32_t amount, void* workspace,
+            int32_t* out_items, void* out_scores, void* stream);
+
+/* ---------------- BaselineModel (bias-only), baseline_model.py ---------- */
+
+/* One bias-SGD epoch over a conflict-free batch schedule: replaces one epoch
+ * of baseline_model.py `_sgd` (:250-266).  Same schedule contract as
+ * mf_sgd_epoch. */
+int mf_bias_sgd_epoch(const int32_t* user_ids, const int32_t* item_ids,
+                      const void* ratings, int64_t n_ratings,
+                      const int32_t* order, const int64_t* batch_offsets,
+                      const int32_t* batch_seq, int32_t n_batches,
+                      double global_mean, void* user_biases,
+                      void* item_biases, int32_t dtype, double lr, double reg,
+                      int32_t update_user_params, int32_t update_item_params,
+                      void* stream);
+
+/* Bias-model SSE, replaces baseline_model.py `_calculate_rmse` (:183-212). */
+int mf_bias_sse(const int32_t* user_ids, const int32_t* item_ids,
+                const void* ratings, int64_t n_ratings, double global_mean,
+                const void* user_biases, const void* item_biases,
+                int32_t dtype, void* workspace, double* sse_out, void* stream);
+
+/*
+ * One alternating-least-squares epoch of the bias model: replaces one epoch
+ * of baseline_model.py `_als` (:326-348).  Sums are taken per id in the
+ * reference's order through CSR lists:
+ *   user_ptr (n_users+1) / user_list: rating indices of each user, ascending
+ *   item_ptr (n_items+1) / item_list: rating indices of each item, ascending
+ * (all device, int64 ptr / int32 list), so results are bit-identical to the
+ * sequential reference loop.  Counts are the list lengths (:317-323).
+ */
+int mf_bias_als_epoch(const int32_t* user_ids, const int32_t* item_ids,
+                      const void* ratings, double global_mean,
+                      void* user_biases, void* item_biases, int32_t n_users,
+                      int32_t n_items, const int64_t* user_ptr,
+                      const int32_t* user_list, const int64_t* item_ptr,
+                      const int32_t* item_list, int32_t dtype, double reg,
+                      void* stream);
+
+/* Bias-model prediction, replaces baseline_model.py `_predict` (:365-417). */
+int mf_bias_predict(const int32_t* user_ids, const int32_t* item_ids,
+                    int64_t n_pairs, double global_mean,
+                    const void* user_biases, const void* item_biases,
+                    int32_t dtype, double min_rating, double max_rating,
+                    int32_t bound_ratings, void* out, void* stream);
+
+/* ---------------- host-side schedulers (no GPU) -------------------------- */
+
+/*
+ * Exact-order schedule.  Given the visit order of one epoch (the row order
+ * of X after `np.random.shuffle(X)`, kernel_matrix_factorization.py:371),
+ * assign every rating the level 1 + max(level of the previous rating of the
+ * same user, ... of the same item) and group positions by level.  Applying
+ * the levels in increasing order (mf_sgd_epoch) is bit-for-bit the
+ * reference's sequential sweep.  use_user / use_item drop a row family
+ * from the conflict test when it is not written (update_users passes
+ * use_item = 0, kernel_matrix_factorization.py:234).
+ *
+ *   order            host, nullable, n: visit order (rating indices)
+ *   sched_out        host, n: rating indices grouped by level, each level
+ *                    in visit order
+ *   level_offsets    host, capacity `offsets_cap` (>= n_levels + 1)
+ *   n_levels_out     host
+ */
+int mf_sched_levels(const int32_t* user_ids, const int32_t* item_ids,
+                    int64_t n, const int64_t* order, int32_t n_users,
+                    int32_t n_items, int32_t use_user, int32_t use_item,
+                    int32_t* sched_out, int64_t* level_offsets,
+                    int64_t offsets_cap, int32_t* n_levels_out);
+
+/*
+ * Throughput schedule.  Greedy edge colouring of the bipartite rating graph
+ * (no two ratings of one colour share a user or an item), ratings visited
+ * item by item.  Output: rating indices grouped by colour, each colour sorted
+ * by item id (so a batch walks Q in address order), plus colour offsets.
+ * Any order of colours is a valid sequential order of the ratings.
+ *   colour count <= max user degree + max item degree - 1 (offsets_cap must
+ *   be at least that + 1).
+ */
+int mf_sched_color(const int32_t* user_ids, const int32_t* item_ids,
+                   int64_t n, int32_t n_users, int32_t n_items,
+                   int32_t* sched_out, int64_t* color_offsets,
+                   int64_t offsets_cap, int32_t* n_colors_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MF_HIP_H */

@@ -1,0 +1,25 @@
+"""matrix_factorization -- MI355X-native drop-in for the SGD path of
+SHEEPididoo/matrix-factorization.
+
+Same public names as the reference package for the path this build covers
+(matrix_factorization/__init__.py:1-16 of the reference): KernelMF and
+BaselineModel train on the GPU through libmf_hip.so (hand-written gfx950
+kernels behind a C ABI, include/mf_hip.h); RecommenderBase and
+train_update_test_split are the host-side surface around them.  The
+neighbourhood and content-based models of the reference are outside this
+build's scope.
+"""
+
+from .baseline_model import BaselineModel
+from .kernel_matrix_factorization import KernelMF
+from .recommender_base import RecommenderBase
+from .utils import train_update_test_split
+
+__all__ = [
+    "BaselineModel",
+    "KernelMF",
+    "RecommenderBase",
+    "train_update_test_split",
+]
+
+__version__ = "0.1.0"

@@ -1,0 +1,112 @@
+"""ctypes binding of libmf_hip.so (the C ABI declared in include/mf_hip.h).
+
+The shared library is built in-tree (``make -C matrix-factorization_amd/csrc``
+or ``__graft_entry__.build()``).  There is no fallback: if the library is
+missing or fails to load, every entry point raises ``MFLibraryError``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MF_HIP_LIB", os.path.join(_HERE, "libmf_hip.so"))
+
+MF_F32, MF_F64 = 0, 1
+MF_LINEAR, MF_SIGMOID, MF_RBF = 0, 1, 2
+MF_FLAG_XCD_SWIZZLE = 1
+MF_ERR_CAPACITY = 3
+KERNEL_CODES = {"linear": MF_LINEAR, "sigmoid": MF_SIGMOID, "rbf": MF_RBF}
+
+_P = ctypes.c_void_p
+_I32 = ctypes.c_int32
+_I64 = ctypes.c_int64
+_F64 = ctypes.c_double
+_PD = ctypes.POINTER(ctypes.c_double)
+
+# name -> (restype, argtypes); mirrors include/mf_hip.h one to one
+SIGNATURES = {
+    "mf_last_error": (ctypes.c_char_p, []),
+    "mf_abi_version": (ctypes.c_int, []),
+    "mf_max_factors": (ctypes.c_int, []),
+    "mf_sgd_epoch": (ctypes.c_int, [
+        _P, _P, _P, _I64, _P, _P, _P, _I32,          # ids, ratings, n, order, offs, seq, nb
+        _F64, _P, _P, _P, _P,                         # mu, bu, bi, P, Q
+        _I32, _I32, _I32,                             # n_users, n_items, k
+        _I32, _I32, _F64, _F64, _F64, _F64, _F64,     # kernel dtype gamma lr reg min max
+        _I32, _I32, _I32, _P, _PD]),                  # upd_u upd_i flags stream kernel_ms
+    "mf_sse_workspace_bytes": (ctypes.c_size_t, [_I64]),
+    "mf_sse": (ctypes.c_int, [
+        _P, _P, _P, _I64, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _F64, _F64,
+        _F64, _P, _P, _P]),
+    "mf_predict": (ctypes.c_int, [
+        _P, _P, _I64, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _F64, _F64,
+        _F64, _I32, _P, _P]),
+    "mf_topk_workspace_bytes": (ctypes.c_size_t, [_I32, _I32, _I32]),
+    "mf_topk": (ctypes.c_int, [
+        _P, _I32, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _F64, _F64,
+        _F64, _P, _I32, _P, _P, _P, _P]),
+    "mf_bias_sgd_epoch": (ctypes.c_int, [
+        _P, _P, _P, _I64, _P, _P, _P, _I32, _F64, _P, _P, _I32, _F64, _F64,
+        _I32, _I32, _P]),
+    "mf_bias_sse": (ctypes.c_int, [
+        _P, _P, _P, _I64, _F64, _P, _P, _I32, _P, _P, _P]),
+    "mf_bias_als_epoch": (ctypes.c_int, [
+        _P, _P, _P, _F64, _P, _P, _I32, _I32, _P, _P, _P, _P, _I32, _F64, _P]),
+    "mf_bias_predict": (ctypes.c_int, [
+        _P, _P, _I64, _F64, _P, _P, _I32, _F64, _F64, _I32, _P, _P]),
+    "mf_sched_levels": (ctypes.c_int, [
+        _P, _P, _I64, _P, _I32, _I32, _I32, _I32, _P, _P, _I64, _P]),
+    "mf_sched_color": (ctypes.c_int, [
+        _P, _P, _I64, _I32, _I32, _P, _P, _I64, _P]),
+}
+
+
+class MFLibraryError(RuntimeError):
+    """libmf_hip.so is missing, failed to load, or returned an error."""
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libmf_hip.so once; raise MFLibraryError if it is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise MFLibraryError(
+                    f"{LIB_PATH} not found: build it with "
+                    "`make -C matrix-factorization_amd/csrc` (hipcc, gfx950)")
+            try:
+                lib = ctypes.CDLL(LIB_PATH)
+            except OSError as e:  # pragma: no cover - environment specific
+                raise MFLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def last_error() -> str:
+    msg = load().mf_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise MFLibraryError(f"{what} failed (code {rc}): {last_error()}")
+
+
+def call(name: str, *args) -> int:
+    """Call an entry point and raise on a non-zero status."""
+    rc = getattr(load(), name)(*args)
+    check(rc, name)
+    return rc

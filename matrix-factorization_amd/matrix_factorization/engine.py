@@ -1,0 +1,397 @@
+"""Device-side training state: ratings and parameters resident in HBM.
+
+This is the layer the reference implements as numba functions
+(``_sgd`` / ``_calculate_rmse`` / ``_predict``,
+kernel_matrix_factorization.py:240-541, and their bias-only twins in
+baseline_model.py:183-417).  Here the ratings (SoA: int32 user, int32 item,
+dtype rating) and the parameters (P, Q, b_u, b_i) live in torch-ROCm tensors
+on one GPU and every sweep is a call into libmf_hip.so.
+
+Two epoch schedules:
+
+``exact``    the reference's visit order.  The caller draws the epoch's
+             permutation exactly as the reference does (``np.random.shuffle``
+             on the rating rows, kernel_matrix_factorization.py:371); the
+             host scheduler cuts it into dependency levels and the GPU applies
+             level after level -- bit-for-bit the sequential sweep, up to the
+             summation order of the k-long dot products.
+``colored``  throughput.  Ratings are edge-coloured once per fit (every
+             colour is a matching: no shared user or item), stored colour-major
+             and item-sorted in HBM; each epoch applies the colours in a fresh
+             random order, i.e. a different valid sequential order per epoch.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_VOID = ctypes.c_void_p
+
+DTYPES = {
+    "float32": (torch.float32, np.float32, _lib.MF_F32),
+    "float64": (torch.float64, np.float64, _lib.MF_F64),
+}
+
+
+def canonical_dtype(dtype) -> str:
+    name = np.dtype(dtype).name
+    if name not in DTYPES:
+        raise ValueError(f"dtype must be float32 or float64, got {dtype!r}")
+    return name
+
+
+def resolve_device(device=None) -> torch.device:
+    """The GPU the engine runs on.  There is no CPU path."""
+    if device is None:
+        if not torch.cuda.is_available():
+            raise _lib.MFLibraryError(
+                "no HIP device visible: matrix_factorization trains on an "
+                "AMD Instinct GPU (gfx950) through libmf_hip.so")
+        return torch.device("cuda", torch.cuda.current_device())
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise ValueError(f"device must be a HIP ('cuda') device, got {device!r}")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
+def _tp(t: Optional[torch.Tensor]):
+    if t is None or t.numel() == 0:
+        return None
+    return _VOID(t.data_ptr())
+
+
+def _np(a: Optional[np.ndarray]):
+    if a is None:
+        return None
+    return a.ctypes.data_as(_VOID)
+
+
+# ------------------------------------------------------------ schedulers
+def sched_levels(u: np.ndarray, i: np.ndarray, order: Optional[np.ndarray],
+                 n_users: int, n_items: int, use_user: bool = True,
+                 use_item: bool = True) -> Tuple[np.ndarray, np.ndarray]:
+    """Exact-order batches: (rating indices grouped by level, level offsets)."""
+    n = len(u)
+    u = np.ascontiguousarray(u, np.int32)
+    i = np.ascontiguousarray(i, np.int32)
+    if order is not None:
+        order = np.ascontiguousarray(order, np.int64)
+    sched = np.empty(n, np.int32)
+    offs = np.empty(n + 1, np.int64)
+    nl = ctypes.c_int32(0)
+    _lib.call("mf_sched_levels", _np(u), _np(i), n, _np(order), n_users,
+              n_items, int(use_user), int(use_item), _np(sched), _np(offs),
+              n + 1, ctypes.byref(nl))
+    return sched, offs[: nl.value + 1].copy()
+
+
+def sched_color(u: np.ndarray, i: np.ndarray, n_users: int,
+                n_items: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Edge-colouring batches: (rating indices colour-major, colour offsets)."""
+    n = len(u)
+    u = np.ascontiguousarray(u, np.int32)
+    i = np.ascontiguousarray(i, np.int32)
+    if n == 0:
+        return np.empty(0, np.int32), np.zeros(1, np.int64)
+    cap = int(np.bincount(u, minlength=n_users).max()
+              + np.bincount(i, minlength=n_items).max() + 1)
+    sched = np.empty(n, np.int32)
+    offs = np.empty(cap, np.int64)
+    nc = ctypes.c_int32(0)
+    _lib.call("mf_sched_color", _np(u), _np(i), n, n_users, n_items,
+              _np(sched), _np(offs), cap, ctypes.byref(nc))
+    return sched, offs[: nc.value + 1].copy()
+
+
+# --------------------------------------------------------------- engine
+class SGDEngine:
+    """Ratings + factor-model parameters on one GPU.
+
+    ``kernel`` is ``"linear" | "sigmoid" | "rbf"`` (KernelMF) or ``"bias"``
+    (BaselineModel: no factor matrices).
+    """
+
+    def __init__(self, u: np.ndarray, i: np.ndarray, r: np.ndarray,
+                 n_users: int, n_items: int, n_factors: int, kernel: str,
+                 dtype="float64", device=None, gamma: float = 0.0,
+                 min_rating: float = 0.0, max_rating: float = 5.0,
+                 global_mean: float = 0.0):
+        self.dev = resolve_device(device)
+        self.dtype = canonical_dtype(dtype)
+        self.tdt, self.ndt, self.dcode = DTYPES[self.dtype]
+        self.kernel = kernel
+        self.bias_only = kernel == "bias"
+        if not self.bias_only:
+            if kernel not in _lib.KERNEL_CODES:
+                raise ValueError(f"unknown kernel {kernel!r}")
+            self.kcode = _lib.KERNEL_CODES[kernel]
+            kmax = _lib.load().mf_max_factors()
+            if not 0 <= n_factors <= kmax:
+                raise ValueError(f"n_factors must be in [0, {kmax}], got {n_factors}")
+        _lib.load()
+        self.n = int(len(u))
+        self.n_users, self.n_items = int(n_users), int(n_items)
+        self.k = int(n_factors)
+        self.gamma = float(gamma)
+        self.min_rating, self.max_rating = float(min_rating), float(max_rating)
+        self.global_mean = float(global_mean)
+        self.u_host = np.ascontiguousarray(u, np.int32)
+        self.i_host = np.ascontiguousarray(i, np.int32)
+        self.r_host = np.ascontiguousarray(r, self.ndt)
+        if self.n and (self.u_host.min() < 0 or self.u_host.max() >= n_users
+                       or self.i_host.min() < 0 or self.i_host.max() >= n_items):
+            raise ValueError("rating ids outside [0, n_users) x [0, n_items)")
+        self._upload_triples(self.u_host, self.i_host, self.r_host)
+        self.colored = None          # (offsets,) once prepare_colored() ran
+        ws = max(_lib.load().mf_sse_workspace_bytes(self.n), 8)
+        self.ws = torch.empty((ws + 7) // 8, dtype=torch.float64, device=self.dev)
+        self.sse_buf = torch.zeros(16, dtype=torch.float64, device=self.dev)
+        self.P = self.Q = self.bu = self.bi = None
+
+    # ---------------------------------------------------------- plumbing
+    @property
+    def stream(self):
+        return _VOID(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def _upload_triples(self, u, i, r):
+        self.u = torch.from_numpy(u).to(self.dev)
+        self.i = torch.from_numpy(i).to(self.dev)
+        self.r = torch.from_numpy(r).to(self.dev)
+
+    def _dev(self, a, shape) -> torch.Tensor:
+        if isinstance(a, torch.Tensor):
+            t = a.to(device=self.dev, dtype=self.tdt)
+        else:
+            t = torch.from_numpy(np.ascontiguousarray(a, self.ndt)).to(self.dev)
+        t = t.reshape(shape).contiguous()
+        return t
+
+    def load_params(self, P=None, Q=None, bu=None, bi=None) -> None:
+        """Upload parameters (NumPy or torch); None keeps the current one."""
+        if P is not None:
+            self.P = self._dev(P, (self.n_users, self.k))
+        if Q is not None:
+            self.Q = self._dev(Q, (self.n_items, self.k))
+        if bu is not None:
+            self.bu = self._dev(bu, (self.n_users,))
+        if bi is not None:
+            self.bi = self._dev(bi, (self.n_items,))
+
+    def params_numpy(self):
+        """(P, Q, b_u, b_i) as float64 host arrays (synchronises)."""
+        out = []
+        for t in (self.P, self.Q, self.bu, self.bi):
+            out.append(None if t is None else t.cpu().numpy().astype(np.float64))
+        return tuple(out)
+
+    def _ensure_sse_slots(self, n):
+        if self.sse_buf.numel() < n:
+            buf = torch.zeros(max(n, 2 * self.sse_buf.numel()), dtype=torch.float64,
+                              device=self.dev)
+            buf[: self.sse_buf.numel()] = self.sse_buf
+            self.sse_buf = buf
+
+    # ---------------------------------------------------------- schedules
+    def prepare_colored(self) -> int:
+        """Colour the ratings once and store them colour-major in HBM.
+
+        Returns the number of colours (batches per epoch)."""
+        sched, offs = sched_color(self.u_host, self.i_host, self.n_users, self.n_items)
+        self.u_host = self.u_host[sched]
+        self.i_host = self.i_host[sched]
+        self.r_host = self.r_host[sched]
+        self._upload_triples(self.u_host, self.i_host, self.r_host)
+        self.colored = offs
+        return len(offs) - 1
+
+    def epoch_exact(self, order: np.ndarray, lr: float, reg: float,
+                    update_user: bool = True, update_item: bool = True,
+                    timing: bool = False) -> Optional[float]:
+        """One epoch in the given visit order (rating indices)."""
+        if self.colored is not None:
+            raise RuntimeError("engine holds colour-major ratings; exact order "
+                               "needs the original order")
+        sched, offs = sched_levels(self.u_host, self.i_host, order, self.n_users,
+                                   self.n_items, update_user, update_item)
+        idx = torch.from_numpy(sched).to(self.dev)
+        return self._run(idx, offs, None, lr, reg, update_user, update_item, 0, timing)
+
+    def epoch_colored(self, seq: Optional[np.ndarray], lr: float, reg: float,
+                      update_user: bool = True, update_item: bool = True,
+                      flags: int = _lib.MF_FLAG_XCD_SWIZZLE,
+                      timing: bool = False) -> Optional[float]:
+        """One epoch applying the colours in order ``seq`` (a permutation)."""
+        if self.colored is None:
+            raise RuntimeError("call prepare_colored() first")
+        if seq is not None:
+            seq = np.ascontiguousarray(seq, np.int32)
+        return self._run(None, self.colored, seq, lr, reg, update_user,
+                         update_item, flags, timing)
+
+    def _run(self, idx, offs, seq, lr, reg, update_user, update_item, flags, timing):
+        nb = len(offs) - 1
+        ms = ctypes.c_double(0.0) if timing else None
+        with torch.cuda.device(self.dev):
+            if self.bias_only:
+                _lib.call("mf_bias_sgd_epoch", _tp(self.u), _tp(self.i), _tp(self.r),
+                          self.n, _tp(idx), _np(offs), _np(seq), nb,
+                          self.global_mean, _tp(self.bu), _tp(self.bi), self.dcode,
+                          float(lr), float(reg), int(update_user), int(update_item),
+                          self.stream)
+                return None
+            _lib.call("mf_sgd_epoch", _tp(self.u), _tp(self.i), _tp(self.r), self.n,
+                      _tp(idx), _np(offs), _np(seq), nb, self.global_mean,
+                      _tp(self.bu), _tp(self.bi), _tp(self.P), _tp(self.Q),
+                      self.n_users, self.n_items, self.k, self.kcode, self.dcode,
+                      self.gamma, float(lr), float(reg), self.min_rating,
+                      self.max_rating, int(update_user), int(update_item), int(flags),
+                      self.stream, ctypes.byref(ms) if timing else None)
+        return ms.value if timing else None
+
+    # ---------------------------------------------------------- read-only
+    def sse_async(self, slot: int) -> None:
+        """Enqueue the training SSE into device slot ``slot``."""
+        self._ensure_sse_slots(slot + 1)
+        out = _VOID(self.sse_buf.data_ptr() + 8 * slot)
+        with torch.cuda.device(self.dev):
+            if self.bias_only:
+                _lib.call("mf_bias_sse", _tp(self.u), _tp(self.i), _tp(self.r), self.n,
+                          self.global_mean, _tp(self.bu), _tp(self.bi), self.dcode,
+                          _tp(self.ws), out, self.stream)
+            else:
+                _lib.call("mf_sse", _tp(self.u), _tp(self.i), _tp(self.r), self.n,
+                          self.global_mean, _tp(self.bu), _tp(self.bi), _tp(self.P),
+                          _tp(self.Q), self.k, self.kcode, self.dcode, self.gamma,
+                          self.min_rating, self.max_rating, _tp(self.ws), out,
+                          self.stream)
+
+    def sse_values(self, n_slots: int) -> np.ndarray:
+        return self.sse_buf[:n_slots].cpu().numpy().copy()
+
+    def rmse_values(self, n_slots: int) -> list:
+        if self.n == 0:
+            return [float("nan")] * n_slots
+        sse = self.sse_values(n_slots)
+        return [float(np.sqrt(s / self.n)) for s in sse]
+
+    def predict(self, u: np.ndarray, i: np.ndarray, bound: bool) -> np.ndarray:
+        """Predictions for id pairs (-1 = unknown), float64 host array."""
+        n = len(u)
+        if n == 0:
+            return np.empty(0, np.float64)
+        ud = torch.from_numpy(np.ascontiguousarray(u, np.int32)).to(self.dev)
+        idd = torch.from_numpy(np.ascontiguousarray(i, np.int32)).to(self.dev)
+        out = torch.empty(n, dtype=self.tdt, device=self.dev)
+        with torch.cuda.device(self.dev):
+            if self.bias_only:
+                _lib.call("mf_bias_predict", _tp(ud), _tp(idd), n, self.global_mean,
+                          _tp(self.bu), _tp(self.bi), self.dcode, self.min_rating,
+                          self.max_rating, int(bound), _tp(out), self.stream)
+            else:
+                _lib.call("mf_predict", _tp(ud), _tp(idd), n, self.global_mean,
+                          _tp(self.bu), _tp(self.bi), _tp(self.P), _tp(self.Q), self.k,
+                          self.kcode, self.dcode, self.gamma, self.min_rating,
+                          self.max_rating, int(bound), _tp(out), self.stream)
+        return out.cpu().numpy().astype(np.float64)
+
+    def topk(self, users: np.ndarray, amount: int,
+             exclude: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """Best ``amount`` items per internal user id: (item ids, scores)."""
+        if self.bias_only:
+            raise NotImplementedError("top-k is implemented for factor models")
+        nq = len(users)
+        items = torch.empty((nq, amount), dtype=torch.int32, device=self.dev)
+        scores = torch.empty((nq, amount), dtype=self.tdt, device=self.dev)
+        if nq == 0 or amount == 0:
+            return items.cpu().numpy(), scores.cpu().numpy().astype(np.float64)
+        ud = torch.from_numpy(np.ascontiguousarray(users, np.int32)).to(self.dev)
+        ex = None
+        if exclude is not None:
+            ex = torch.from_numpy(np.ascontiguousarray(exclude, np.uint8)).to(self.dev)
+        wsb = _lib.load().mf_topk_workspace_bytes(nq, self.n_items, amount)
+        ws = torch.empty(max(wsb, 8), dtype=torch.uint8, device=self.dev)
+        with torch.cuda.device(self.dev):
+            _lib.call("mf_topk", _tp(ud), nq, self.global_mean, _tp(self.bu),
+                      _tp(self.bi), _tp(self.P), _tp(self.Q), self.n_items, self.k,
+                      self.kcode, self.dcode, self.gamma, self.min_rating,
+                      self.max_rating, _tp(ex), amount, _tp(ws), _tp(items),
+                      _tp(scores), self.stream)
+        return items.cpu().numpy(), scores.cpu().numpy().astype(np.float64)
+
+
+class BiasALS:
+    """CSR lists for the bias-model ALS (baseline_model.py:313-348)."""
+
+    def __init__(self, engine: SGDEngine):
+        e = engine
+        n = e.n
+
+        def csr(ids, m):
+            cnt = np.bincount(ids, minlength=m).astype(np.int64)
+            ptr = np.zeros(m + 1, np.int64)
+            np.cumsum(cnt, out=ptr[1:])
+            lst = np.argsort(ids, kind="stable").astype(np.int32)   # row order kept
+            return ptr, lst
+
+        up, ul = csr(e.u_host, e.n_users) if n else (np.zeros(e.n_users + 1, np.int64), np.zeros(0, np.int32))
+        ip, il = csr(e.i_host, e.n_items) if n else (np.zeros(e.n_items + 1, np.int64), np.zeros(0, np.int32))
+        to = lambda a: torch.from_numpy(a).to(e.dev)  # noqa: E731
+        self.e = e
+        self.up, self.ul, self.ip, self.il = to(up), to(ul), to(ip), to(il)
+
+    def epoch(self, reg: float) -> None:
+        e = self.e
+        with torch.cuda.device(e.dev):
+            _lib.call("mf_bias_als_epoch", _tp(e.u), _tp(e.i), _tp(e.r), e.global_mean,
+                      _tp(e.bu), _tp(e.bi), e.n_users, e.n_items, _tp(self.up),
+                      _tp(self.ul), _tp(self.ip), _tp(self.il), e.dcode, float(reg),
+                      e.stream)
+
+
+def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
+               reg: float, update_user: bool = True, update_item: bool = True,
+               verbose: int = 0, rng_order: Optional[np.ndarray] = None,
+               on_epoch=None) -> list:
+    """Run ``n_epochs`` of SGD + training-RMSE exactly as ``_sgd`` does
+    (kernel_matrix_factorization.py:367-445).  Returns train_rmse (list).
+
+    exact:   draws ``np.random.shuffle`` on the row order every epoch
+             (the reference's RNG stream, :371);
+    colored: draws ``np.random.permutation(n_colours)`` every epoch.
+    """
+    if schedule == "exact":
+        order = (np.arange(engine.n, dtype=np.int64) if rng_order is None
+                 else rng_order)
+    elif schedule == "colored":
+        if engine.colored is None:
+            engine.prepare_colored()
+        nb = len(engine.colored) - 1
+    else:
+        raise ValueError(f"schedule must be 'exact' or 'colored', got {schedule!r}")
+    train_rmse = []
+    for epoch in range(n_epochs):
+        if schedule == "exact":
+            np.random.shuffle(order)
+            engine.epoch_exact(order, lr, reg, update_user, update_item)
+        else:
+            seq = np.random.permutation(nb).astype(np.int32)
+            engine.epoch_colored(seq, lr, reg, update_user, update_item)
+        engine.sse_async(epoch)
+        if verbose == 1:
+            rmse = engine.rmse_values(epoch + 1)[epoch]
+            train_rmse.append(rmse)
+            print("Epoch ", epoch + 1, "/", n_epochs, " -  train_rmse:", rmse)
+        if on_epoch is not None:
+            on_epoch(epoch)
+    if verbose != 1:
+        train_rmse = engine.rmse_values(n_epochs)
+    return train_rmse

@@ -1,0 +1,148 @@
+"""Estimator base class: the reference's public surface, GPU underneath.
+
+Mirrors ``RecommenderBase`` (recommender_base.py:14-271): an sklearn
+estimator with id remapping, ``recommend`` and the known-user/item helpers.
+Every random draw happens in the reference's order through NumPy's global
+legacy RandomState (``X.sample(frac=1)`` here, ``np.random.normal`` /
+``np.random.shuffle`` in the subclasses), so ``np.random.seed(s)`` followed by
+the same calls gives the reference's results.
+"""
+
+from __future__ import annotations
+
+from abc import ABCMeta, abstractmethod
+from typing import Any, Tuple, Union
+
+import numpy as np
+import pandas as pd
+from sklearn.base import BaseEstimator, RegressorMixin
+
+
+def _index_of(keys) -> pd.Index:
+    return pd.Index(list(keys))
+
+
+class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
+    """Abstract base of every model (recommender_base.py:14-51).
+
+    Attributes after fit: n_users, n_items, global_mean, user_id_map,
+    item_id_map (dict: external id -> internal id, first-appearance order of
+    the shuffled training data).
+    """
+
+    @abstractmethod
+    def __init__(self, min_rating: float = 0, max_rating: float = 5, verbose: int = 0):
+        self.min_rating = min_rating
+        self.max_rating = max_rating
+        self.verbose = verbose
+
+    # ------------------------------------------------ known ids (:53-95)
+    @property
+    def known_users(self):
+        return set(self.user_id_map.keys())
+
+    @property
+    def known_items(self):
+        return set(self.item_id_map.keys())
+
+    def contains_user(self, user_id: Any) -> bool:
+        return user_id in self.user_id_map
+
+    def contains_item(self, item_id: Any) -> bool:
+        return item_id in self.item_id_map
+
+    # ---------------------------------------------------- id remapping
+    @staticmethod
+    def _remap(values: pd.Series, id_map: dict) -> np.ndarray:
+        """External ids -> internal int64 ids, -1 where unknown.
+
+        The maps are built so that the internal id of a key equals its
+        insertion position, which lets pandas' hash index do the lookup."""
+        idx = _index_of(id_map.keys())
+        if len(id_map) and next(reversed(id_map.values())) != len(id_map) - 1:
+            # not positional (never produced by this package); use the dict
+            return values.map(id_map).fillna(-1).to_numpy().astype(np.int64)
+        return idx.get_indexer(values.to_numpy()).astype(np.int64)
+
+    def _preprocess_data(
+        self, X: pd.DataFrame, y: pd.Series = None, type: str = "fit"
+    ) -> Union[pd.DataFrame, Tuple[pd.DataFrame, list, list]]:
+        """recommender_base.py:97-173.
+
+        fit:     duplicate check, ``X.sample(frac=1)`` (one RNG draw), new id
+                 maps in first-appearance order of the shuffled rows;
+        update:  same check and shuffle, drop ratings of unknown items, append
+                 new users to user_id_map (ids max + 1, ...);
+        predict: unknown ids become -1.
+        Returns a frame with int64 user_id / item_id (and rating).
+        """
+        X = X.loc[:, ["user_id", "item_id"]]
+        if type != "predict":
+            X["rating"] = y
+
+        if type in ("fit", "update"):
+            if X.duplicated(subset=["user_id", "item_id"]).sum() != 0:
+                raise ValueError("Duplicate user-item ratings in matrix")
+            X = X.sample(frac=1, replace=False)
+
+        if type == "fit":
+            ucodes, uniq_u = pd.factorize(X["user_id"], sort=False)
+            icodes, uniq_i = pd.factorize(X["item_id"], sort=False)
+            self.user_id_map = {uid: n for n, uid in enumerate(uniq_u)}
+            self.item_id_map = {iid: n for n, iid in enumerate(uniq_i)}
+            self.n_users = len(uniq_u)
+            self.n_items = len(uniq_i)
+            out = pd.DataFrame({"user_id": ucodes.astype(np.int64),
+                                "item_id": icodes.astype(np.int64)}, index=X.index)
+            out["rating"] = X["rating"]
+            return out
+
+        known_users, new_users = [], []
+        if type == "update":
+            X = X[X["item_id"].isin(list(self.item_id_map.keys()))].copy()
+            new_id = max(self.user_id_map.values()) + 1
+            for user in X["user_id"].unique():
+                if user in self.user_id_map:
+                    known_users.append(user)
+                    continue
+                new_users.append(user)
+                self.user_id_map[user] = new_id
+                new_id += 1
+
+        out = pd.DataFrame({"user_id": self._remap(X["user_id"], self.user_id_map),
+                            "item_id": self._remap(X["item_id"], self.item_id_map)},
+                           index=X.index)
+        if type != "predict":
+            out["rating"] = X["rating"]
+        if type == "update":
+            return out, known_users, new_users
+        return out
+
+    @abstractmethod
+    def fit(self, X: pd.DataFrame, y: pd.Series):
+        return self
+
+    @abstractmethod
+    def predict(self, X: pd.DataFrame, bound_ratings: bool = True) -> list:
+        return []
+
+    def recommend(self, user: Any, amount: int = 10, items_known: list = None,
+                  include_user: bool = True, bound_ratings: bool = True) -> pd.DataFrame:
+        """Top ``amount`` unseen items for ``user``, best first
+        (recommender_base.py:214-271): every candidate is scored with
+        ``predict(bound_ratings=False)`` on the GPU and ranked by pandas'
+        ``sort_values`` exactly as the reference ranks them."""
+        items = list(self.item_id_map.keys())
+        if items_known is not None:
+            known = set(items_known)
+            items = [item for item in items if item not in known]
+        recs = pd.DataFrame({"user_id": user, "item_id": items})
+        recs["rating_pred"] = self.predict(X=recs, bound_ratings=False)
+        recs.sort_values(by="rating_pred", ascending=False, inplace=True)
+        recs = recs.head(amount).copy()
+        if bound_ratings:
+            recs["rating_pred"] = recs["rating_pred"].clip(lower=self.min_rating,
+                                                           upper=self.max_rating)
+        if not include_user:
+            recs.drop(["user_id"], axis="columns", inplace=True)
+        return recs

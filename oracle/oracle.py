@@ -87,13 +87,15 @@ def _c(a, dt):
 def sgd_pass(u, i, r, mu, bu, bi, P, Q, kernel="linear", gamma=0.0, lr=0.01,
              reg=0.02, min_rating=0.0, max_rating=5.0, order=None,
              update_user=True, update_item=True):
-    """One sequential sweep in ``order``; mutates bu, bi, P, Q (float64, C)."""
+    """One sequential sweep over ``order`` (rating indices; default all
+    ratings in row order); mutates bu, bi, P, Q (float64, C-contiguous)."""
     for a in (bu, bi, P, Q):
         assert a.dtype == np.float64 and a.flags.c_contiguous
     u = _c(u, np.int32); i = _c(i, np.int32); r = _c(r, np.float64)
     order = None if order is None else _c(order, np.int64)
     k = P.shape[1] if P.ndim == 2 else 0
-    lib().oracle_sgd_pass(_p(u), _p(i), _p(r), len(u), _p(order), float(mu),
+    steps = len(u) if order is None else len(order)
+    lib().oracle_sgd_pass(_p(u), _p(i), _p(r), steps, _p(order), float(mu),
                           _p(bu), _p(bi), _p(P), _p(Q), k, KERNELS[kernel],
                           float(gamma), float(lr), float(reg),
                           float(min_rating), float(max_rating - min_rating),
@@ -132,7 +134,8 @@ def bias_sgd_pass(u, i, r, mu, bu, bi, lr, reg, order=None, update_user=True,
                   update_item=True):
     u = _c(u, np.int32); i = _c(i, np.int32); r = _c(r, np.float64)
     order = None if order is None else _c(order, np.int64)
-    lib().oracle_bias_sgd_pass(_p(u), _p(i), _p(r), len(u), _p(order),
+    steps = len(u) if order is None else len(order)
+    lib().oracle_bias_sgd_pass(_p(u), _p(i), _p(r), steps, _p(order),
                                float(mu), _p(bu), _p(bi), float(lr),
                                float(reg), int(update_user), int(update_item))
 

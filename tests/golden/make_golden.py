@@ -120,10 +120,10 @@ def kernel_case(ref, name, df, seed, hp, n_test=200, rec_users=(), out=None):
         user_ids=np.asarray(list(m.user_id_map.keys()), np.int64),
         item_ids=np.asarray(list(m.item_id_map.keys()), np.int64),
         global_mean=np.float64(m.global_mean),
-        user_biases=np.asarray(m.user_biases, np.float64),
-        item_biases=np.asarray(m.item_biases, np.float64),
-        user_features=np.asarray(m.user_features, np.float64),
-        item_features=np.asarray(m.item_features, np.float64),
+        user_biases=np.array(m.user_biases, np.float64, copy=True),
+        item_biases=np.array(m.item_biases, np.float64, copy=True),
+        user_features=np.array(m.user_features, np.float64, copy=True),
+        item_features=np.array(m.item_features, np.float64, copy=True),
         train_rmse=np.asarray(m.train_rmse, np.float64),
         gamma=np.float64(m.gamma),
         test_user=T["user_id"].to_numpy(np.int64),
@@ -175,10 +175,10 @@ def case_update(ref, name):
         item_ids=np.asarray(list(m.item_id_map.keys()), np.int64),
         n_users=np.int64(m.n_users),
         global_mean=np.float64(m.global_mean),
-        user_biases=np.asarray(m.user_biases, np.float64),
-        item_biases=np.asarray(m.item_biases, np.float64),
-        user_features=np.asarray(m.user_features, np.float64),
-        item_features=np.asarray(m.item_features, np.float64),
+        user_biases=np.array(m.user_biases, np.float64, copy=True),
+        item_biases=np.array(m.item_biases, np.float64, copy=True),
+        user_features=np.array(m.user_features, np.float64, copy=True),
+        item_features=np.array(m.item_features, np.float64, copy=True),
         train_rmse=np.asarray(m.train_rmse, np.float64),
         pred_test=pred,
     )
@@ -202,8 +202,8 @@ def case_baseline(ref, method):
         user_ids=np.asarray(list(m.user_id_map.keys()), np.int64),
         item_ids=np.asarray(list(m.item_id_map.keys()), np.int64),
         global_mean=np.float64(m.global_mean),
-        user_biases=np.asarray(m.user_biases, np.float64),
-        item_biases=np.asarray(m.item_biases, np.float64),
+        user_biases=np.array(m.user_biases, np.float64, copy=True),
+        item_biases=np.array(m.item_biases, np.float64, copy=True),
         train_rmse=np.asarray(m.train_rmse, np.float64),
         test_user=T["user_id"].to_numpy(np.int64),
         test_item=T["item_id"].to_numpy(np.int64),
@@ -219,7 +219,7 @@ def case_baseline(ref, method):
         out.update(upd_user=Xn["user_id"].to_numpy(np.int64),
                    upd_item=Xn["item_id"].to_numpy(np.int64),
                    upd_rating=yn.to_numpy(np.float64),
-                   upd_user_biases=np.asarray(m.user_biases, np.float64),
+                   upd_user_biases=np.array(m.user_biases, np.float64, copy=True),
                    upd_train_rmse=np.asarray(m.train_rmse, np.float64))
     return out
 

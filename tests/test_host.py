@@ -1,0 +1,348 @@
+"""CPU tests of the host side: C-ABI exports, schedulers, estimator logic.
+
+No GPU: the estimator flows (RNG order, id maps, update_users bookkeeping,
+batch schedules) run here against a test double of the device engine whose
+sweeps are the CPU oracle.  The double exists only in this file; the product
+path has no CPU fallback (see test_product_has_no_cpu_path).
+"""
+
+import ctypes
+import os
+import re
+
+import numpy as np
+import pandas as pd
+import pytest
+
+import oracle
+from conftest import ROOT, golden_hp, load_golden
+
+HEADER = os.path.join(ROOT, "include", "mf_hip.h")
+
+
+# ---------------------------------------------------------------- C ABI
+def _declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(mf_\w+)\s*\(", text, flags=re.M)
+    return sorted(set(names))
+
+
+def test_library_exports_every_declared_symbol():
+    from matrix_factorization import _lib
+
+    lib = _lib.load()
+    declared = _declared_functions()
+    assert len(declared) >= 15
+    for name in declared:
+        assert hasattr(lib, name), f"{name} not exported by libmf_hip.so"
+    # the Python binding covers the header one to one
+    assert sorted(_lib.SIGNATURES) == declared
+    assert lib.mf_abi_version() == 1
+    assert lib.mf_max_factors() == 1024
+
+
+def test_library_errors_are_reported():
+    from matrix_factorization import _lib
+
+    lib = _lib.load()
+    offs = np.array([0, 5], np.int64)
+    # n_factors out of range -> MF_ERR_INVALID before any device work
+    rc = lib.mf_sgd_epoch(None, None, None, 0, None, offs.ctypes.data_as(ctypes.c_void_p),
+                          None, 1, 0.0, None, None, None, None, 0, 0, 4096, 0, 0, 0.0,
+                          0.01, 0.02, 0.0, 5.0, 1, 1, 0, None, None)
+    assert rc == 1 and "batch_offsets" in _lib.last_error() or "n_factors" in _lib.last_error()
+    with pytest.raises(_lib.MFLibraryError):
+        _lib.call("mf_predict", None, None, -1, 0.0, None, None, None, None, 8, 0, 0, 0.0,
+                  0.0, 5.0, 1, None, None)
+
+
+# ------------------------------------------------------------ schedulers
+def _random_ratings(seed, nu, ni, nnz):
+    rs = np.random.RandomState(seed)
+    keys = rs.choice(nu * ni, nnz, replace=False)
+    return (keys // ni).astype(np.int32), (keys % ni).astype(np.int32), \
+        rs.randint(1, 6, nnz).astype(np.float64)
+
+
+def test_levels_reproduce_the_sequential_sweep_bit_for_bit():
+    from matrix_factorization.engine import sched_levels
+
+    nu, ni, nnz, k = 60, 45, 1500, 8
+    u, i, r = _random_ratings(0, nu, ni, nnz)
+    rs = np.random.RandomState(1)
+    order = rs.permutation(nnz).astype(np.int64)
+    P = rs.normal(0, 0.1, (nu, k)); Q = rs.normal(0, 0.1, (ni, k))
+    bu = np.zeros(nu); bi = np.zeros(ni)
+    args = dict(kernel="sigmoid", lr=0.05, reg=0.02, min_rating=1, max_rating=5)
+    ref = [a.copy() for a in (bu, bi, P, Q)]
+    oracle.sgd_pass(u, i, r, 3.0, *ref, order=order, **args)
+    sched, offs = sched_levels(u, i, order, nu, ni)
+    assert np.array_equal(np.sort(sched), np.arange(nnz))
+    got = [a.copy() for a in (bu, bi, P, Q)]
+    for b in range(len(offs) - 1):
+        lvl = sched[offs[b]:offs[b + 1]]
+        assert len(np.unique(u[lvl])) == len(lvl) and len(np.unique(i[lvl])) == len(lvl)
+        # inside a level any order gives the same result: use a reversed one
+        oracle.sgd_pass(u, i, r, 3.0, *got, order=lvl[::-1].astype(np.int64), **args)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
+
+
+def test_levels_user_only_for_frozen_items():
+    from matrix_factorization.engine import sched_levels
+
+    u, i, r = _random_ratings(2, 30, 20, 300)
+    order = np.random.RandomState(0).permutation(300)
+    s_full, o_full = sched_levels(u, i, order, 30, 20, True, True)
+    s_user, o_user = sched_levels(u, i, order, 30, 20, True, False)
+    assert len(o_user) - 1 == np.bincount(u).max()
+    assert len(o_user) <= len(o_full)
+
+
+def test_color_schedule_is_a_conflict_free_partition():
+    from matrix_factorization.engine import sched_color
+
+    nu, ni = 400, 150
+    u, i, r = _random_ratings(3, nu, ni, 20000)
+    sched, offs = sched_color(u, i, nu, ni)
+    assert np.array_equal(np.sort(sched), np.arange(len(u)))
+    assert len(offs) - 1 <= np.bincount(u).max() + np.bincount(i).max() - 1
+    for b in range(len(offs) - 1):
+        c = sched[offs[b]:offs[b + 1]]
+        assert len(np.unique(u[c])) == len(c)
+        assert len(np.unique(i[c])) == len(c)
+        assert np.all(np.diff(i[c]) > 0)          # item-sorted inside a colour
+
+
+def test_schedulers_reject_bad_ids():
+    from matrix_factorization import _lib
+    from matrix_factorization.engine import sched_color, sched_levels
+
+    u = np.array([0, 5], np.int32)
+    i = np.array([0, 1], np.int32)
+    with pytest.raises(_lib.MFLibraryError):
+        sched_levels(u, i, None, 3, 3)
+    with pytest.raises(_lib.MFLibraryError):
+        sched_color(u, i, 3, 3)
+
+
+def test_schedulers_handle_empty_input():
+    from matrix_factorization.engine import sched_color, sched_levels
+
+    e = np.zeros(0, np.int32)
+    s, o = sched_levels(e, e, None, 0, 0)
+    assert len(s) == 0 and list(o) == [0]
+    s, o = sched_color(e, e, 0, 0)
+    assert len(s) == 0 and list(o) == [0]
+
+
+# ------------------------------------------------- estimator host logic
+class OracleEngine:
+    """Test double of engine.SGDEngine: same interface, oracle sweeps."""
+
+    def __init__(self, u, i, r, n_users, n_items, n_factors, kernel, dtype="float64",
+                 device=None, gamma=0.0, min_rating=0.0, max_rating=5.0, global_mean=0.0):
+        self.u_host = np.ascontiguousarray(u, np.int32)
+        self.i_host = np.ascontiguousarray(i, np.int32)
+        self.r_host = np.ascontiguousarray(r, np.float64)
+        self.n = len(u)
+        self.n_users, self.n_items, self.k = n_users, n_items, n_factors
+        self.kernel, self.gamma = kernel, gamma
+        self.min_rating, self.max_rating = min_rating, max_rating
+        self.global_mean = global_mean
+        self.colored = None
+        self.sse = {}
+        self.P = self.Q = self.bu = self.bi = None
+
+    def load_params(self, P=None, Q=None, bu=None, bi=None):
+        if P is not None:
+            self.P = np.array(P, np.float64).reshape(self.n_users, self.k)
+        if Q is not None:
+            self.Q = np.array(Q, np.float64).reshape(self.n_items, self.k)
+        if bu is not None:
+            self.bu = np.array(bu, np.float64)
+        if bi is not None:
+            self.bi = np.array(bi, np.float64)
+
+    def params_numpy(self):
+        return tuple(None if a is None else a.copy() for a in (self.P, self.Q, self.bu, self.bi))
+
+    def _kw(self):
+        return dict(kernel=self.kernel, gamma=self.gamma, min_rating=self.min_rating,
+                    max_rating=self.max_rating)
+
+    def epoch_exact(self, order, lr, reg, update_user=True, update_item=True):
+        from matrix_factorization.engine import sched_levels
+
+        sched, offs = sched_levels(self.u_host, self.i_host, order, self.n_users,
+                                   self.n_items, update_user, update_item)
+        for b in range(len(offs) - 1):
+            lvl = sched[offs[b]:offs[b + 1]].astype(np.int64)
+            if self.kernel == "bias":
+                oracle.bias_sgd_pass(self.u_host, self.i_host, self.r_host, self.global_mean,
+                                     self.bu, self.bi, lr, reg, order=lvl,
+                                     update_user=update_user, update_item=update_item)
+            else:
+                oracle.sgd_pass(self.u_host, self.i_host, self.r_host, self.global_mean,
+                                self.bu, self.bi, self.P, self.Q, lr=lr, reg=reg, order=lvl,
+                                update_user=update_user, update_item=update_item,
+                                **self._kw())
+
+    def sse_async(self, slot):
+        if self.kernel == "bias":
+            self.sse[slot] = oracle.bias_sse(self.u_host, self.i_host, self.r_host,
+                                             self.global_mean, self.bu, self.bi)
+        else:
+            self.sse[slot] = oracle.sse(self.u_host, self.i_host, self.r_host,
+                                        self.global_mean, self.bu, self.bi, self.P, self.Q,
+                                        **self._kw())
+
+    def rmse_values(self, n):
+        if self.n == 0:
+            return [float("nan")] * n
+        return [float(np.sqrt(self.sse[s] / self.n)) for s in range(n)]
+
+    def predict(self, u, i, bound):
+        if self.kernel == "bias":
+            out = []
+            for a, b in zip(u, i):
+                p = self.global_mean
+                if a != -1:
+                    p += self.bu[a]
+                if b != -1:
+                    p += self.bi[b]
+                if bound:
+                    p = min(max(p, self.min_rating), self.max_rating) if (
+                        p > self.max_rating or p < self.min_rating) else p
+                out.append(p)
+            return np.array(out)
+        return oracle.predict(u, i, self.global_mean, self.bu, self.bi, self.P, self.Q,
+                              bound=bound, **self._kw())
+
+
+@pytest.fixture
+def cpu_engine(monkeypatch):
+    import matrix_factorization.baseline_model as bm
+    import matrix_factorization.kernel_matrix_factorization as kmf
+
+    monkeypatch.setattr(kmf, "SGDEngine", OracleEngine)
+    monkeypatch.setattr(bm, "SGDEngine", OracleEngine)
+    return OracleEngine
+
+
+@pytest.mark.parametrize("name", ["tiny_linear", "tiny_sigmoid", "tiny_rbf", "tiny_defaults",
+                                  "mid_k100"])
+def test_kernelmf_host_flow_matches_reference(cpu_engine, name, capsys):
+    from matrix_factorization import KernelMF
+
+    d = load_golden(name)
+    hp = golden_hp(d)
+    X = pd.DataFrame({"user_id": d["user_id"], "item_id": d["item_id"]})
+    np.random.seed(int(d["seed"]))
+    m = KernelMF(**hp).fit(X, pd.Series(d["rating"]))
+    out = capsys.readouterr().out
+    if hp.get("verbose", 1) == 1:
+        assert out.count("Epoch ") == hp["n_epochs"]
+    assert list(m.user_id_map) == d["user_ids"].tolist()
+    assert list(m.item_id_map) == d["item_ids"].tolist()
+    for key in ("user_features", "item_features", "user_biases", "item_biases"):
+        assert np.max(np.abs(getattr(m, key) - d[key])) < 1e-12, key
+    assert np.max(np.abs(np.asarray(m.train_rmse) - d["train_rmse"])) < 1e-13
+    T = pd.DataFrame({"user_id": d["test_user"], "item_id": d["test_item"]})
+    assert np.max(np.abs(np.asarray(m.predict(T)) - d["pred_bound"])) < 1e-12
+    assert m.predictions_possible == d["pred_possible"].tolist()
+    df = X.assign(rating=d["rating"])
+    for j, user in enumerate(d["rec_users"]):
+        known = df.loc[df.user_id == user, "item_id"].to_numpy()
+        known = known[: len(known) // 2] if j % 2 == 0 else None
+        rec = m.recommend(user=user, amount=10, items_known=known)
+        assert rec["item_id"].tolist() == d["rec_items"][j].tolist()
+
+
+def test_update_users_host_flow_matches_reference(cpu_engine):
+    from matrix_factorization import KernelMF, train_update_test_split
+
+    d = load_golden("update_users")
+    hp = golden_hp(d)
+    df = pd.DataFrame({"user_id": d["user_id"], "item_id": d["item_id"],
+                       "rating": d["rating"]})
+    np.random.seed(int(d["seed"]))
+    Xi, yi, Xu, yu, Xt, yt = train_update_test_split(df, frac_new_users=0.25)
+    assert Xi.index.tolist() == d["split_train_index"].tolist()
+    assert Xu.index.tolist() == d["split_update_index"].tolist()
+    assert Xt.index.tolist() == d["split_test_index"].tolist()
+    m = KernelMF(**hp).fit(Xi, yi)
+    extra = Xi.loc[d["extra_index"]]
+    Q_before = m.item_features.copy()
+    m.update_users(pd.concat([Xu, extra]), pd.concat([yu, yi.loc[extra.index]]),
+                   lr=0.03, n_epochs=5, verbose=0)
+    assert list(m.user_id_map.values()) == d["user_id_vals"].tolist()
+    assert m.n_users == d["n_users"]
+    assert np.max(np.abs(m.user_features - d["user_features"])) < 1e-12
+    assert np.array_equal(m.item_features, Q_before)          # frozen bit for bit
+    assert np.max(np.abs(m.item_features - d["fit_item_features"])) < 1e-12
+    assert np.max(np.abs(np.asarray(m.predict(Xt)) - d["pred_test"])) < 1e-12
+
+
+@pytest.mark.parametrize("method", ["sgd"])
+def test_baseline_host_flow_matches_reference(cpu_engine, method):
+    from matrix_factorization import BaselineModel
+
+    d = load_golden(f"baseline_{method}")
+    hp = golden_hp(d)
+    X = pd.DataFrame({"user_id": d["user_id"], "item_id": d["item_id"]})
+    np.random.seed(int(d["seed"]))
+    m = BaselineModel(**hp).fit(X, pd.Series(d["rating"]))
+    assert np.array_equal(m.user_biases, d["user_biases"])
+    assert np.array_equal(m.item_biases, d["item_biases"])
+    np.random.seed(int(d["seed"]) + 1)
+    m.update_users(pd.DataFrame({"user_id": d["upd_user"], "item_id": d["upd_item"]}),
+                   pd.Series(d["upd_rating"]), lr=0.05, n_epochs=3)
+    assert np.array_equal(m.user_biases, d["upd_user_biases"])
+
+
+def test_duplicate_ratings_rejected():
+    from matrix_factorization import KernelMF
+
+    X = pd.DataFrame({"user_id": [1, 1], "item_id": [2, 2]})
+    with pytest.raises(ValueError, match="Duplicate"):
+        KernelMF(verbose=0).fit(X, pd.Series([3.0, 4.0]))
+
+
+def test_constructor_validation_and_sklearn_clone():
+    from sklearn.base import clone
+
+    from matrix_factorization import BaselineModel, KernelMF
+
+    with pytest.raises(ValueError, match="Kernel must be"):
+        KernelMF(kernel="poly")
+    with pytest.raises(ValueError):
+        BaselineModel(method="gd")
+    m = KernelMF(n_factors=8, gamma="auto", kernel="rbf", dtype="float32", schedule="colored")
+    assert m.gamma == 1 / 8
+    c = clone(m)
+    assert c.get_params() == m.get_params()
+    assert c.dtype == "float32" and c.schedule == "colored"
+
+
+def test_product_has_no_cpu_path(monkeypatch):
+    """Without a GPU the product path raises instead of computing on the CPU."""
+    import torch
+
+    from matrix_factorization import KernelMF, _lib
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU visible")
+    X = pd.DataFrame({"user_id": [1, 2], "item_id": [2, 3]})
+    with pytest.raises(_lib.MFLibraryError, match="no HIP device"):
+        KernelMF(verbose=0, n_epochs=1).fit(X, pd.Series([3.0, 4.0]))
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    from matrix_factorization import _lib
+
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
+    with pytest.raises(_lib.MFLibraryError, match="not found"):
+        _lib.load()
