@@ -1,0 +1,306 @@
+#!/usr/bin/env python
+"""bench.py -- KernelMF SGD throughput on MI355X (BASELINE.json headline).
+
+Workload (BASELINE.json configs[2], the HBM-roofline headline): synthetic
+1M users x 100K items, 100M unique ratings (1..5 drawn from the ML-100K
+histogram), rank-64 linear-kernel SGD, lr=0.01, reg=0.02, init N(0, 0.1),
+FP32 parameters, colored (conflict-free) schedule.  With --gpus N the same
+100M ratings are user-sharded over N ranks (configs[3]; total work fixed).
+
+One step = one epoch exactly as the reference's `_sgd` runs it
+(kernel_matrix_factorization.py:369-443): the SGD sweep over every rating
+plus the training-RMSE pass.  value = ratings * steps / wall time of the
+timed steps (inputs resident in HBM, max over ranks).
+
+Also reported (rank 0):
+  roofline      SGD-kernel algorithmic bytes (16k+28 B per update, SURVEY
+                8d) / summed kernel time (hipEvents around every launch of
+                the timed steps) against 8 TB/s; `traffic` = measured HBM
+                bytes per launch from rocprofv3 PMC (profiles/) or null;
+  cpu_baseline  the CPU oracle (FP64 C port of the reference loop, 1 core)
+                on a bounded sample: the first colours of epoch 1 (~10M
+                ratings by default), SGD + RMSE over the sample;
+  parity        GPU (FP32) vs oracle (FP64) after that same partial epoch
+                from the same initial state: RMSE over the sample.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "matrix-factorization_amd"))
+
+METRIC = "rating-updates/s + final RMSE, rank-64 SGD, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0
+ML100K_HIST = np.array([6110, 11370, 27145, 34174, 21201], np.float64)
+
+WORKLOADS = {
+    # name: (n_users, n_items, nnz, k, kernel, description)
+    "c3": (1_000_000, 100_000, 100_000_000, 64, "linear",
+           "synthetic 1Mx100K 100M-nnz rank-64 linear SGD"),
+    "c2": (100_000, 10_000, 5_000_000, 32, "sigmoid",
+           "synthetic 100Kx10K 5M-nnz rank-32 sigmoid SGD"),
+    "small": (100_000, 20_000, 4_000_000, 64, "linear",
+              "synthetic 100Kx20K 4M-nnz rank-64 linear SGD (smoke)"),
+}
+
+
+def log(msg: str) -> None:
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def synth(n_users: int, n_items: int, nnz: int, seed: int = 20261015):
+    """nnz unique (user, item) pairs, uniform; ratings from the ML-100K
+    histogram (recommender-evaluation.ipynb:98-102 of the reference)."""
+    rs = np.random.RandomState(seed)
+    extra = max(1000, int(nnz * 2e-3))
+    keys = rs.randint(0, n_users * n_items, size=nnz + extra, dtype=np.int64)
+    keys = np.unique(keys)
+    while len(keys) < nnz:   # top up (never needed at these densities)
+        more = rs.randint(0, n_users * n_items, size=nnz - len(keys) + extra, dtype=np.int64)
+        keys = np.unique(np.concatenate([keys, more]))
+    keep = np.sort(rs.choice(len(keys), nnz, replace=False)) if len(keys) > nnz else None
+    if keep is not None:
+        keys = keys[keep]
+    keys = keys[rs.permutation(nnz)]
+    u = (keys // n_items).astype(np.int32)
+    i = (keys % n_items).astype(np.int32)
+    del keys
+    p = ML100K_HIST / ML100K_HIST.sum()
+    r = (rs.choice(5, size=nnz, p=p) + 1).astype(np.float32)
+    return u, i, r
+
+
+def traffic_from_profiles(workload: str, n_gpus: int):
+    """HBM bytes per SGD launch measured by rocprofv3 PMC passes, if a
+    summary for this workload was committed under profiles/."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(f"{workload}/n{n_gpus}")
+        return None if e is None else float(e["hbm_bytes_per_sgd_launch"])
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--dtype", default="float32", choices=["float32", "float64"])
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--reg", type=float, default=0.02)
+    ap.add_argument("--cpu-sample", type=int, default=10_000_000,
+                    help="ratings in the CPU-oracle sample (0 = skip the CPU leg)")
+    ap.add_argument("--timing-stride", type=int, default=8,
+                    help="bracket every N-th SGD launch of the timed epochs with "
+                         "hipEvents (0 = no kernel timing)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from matrix_factorization import _lib
+    from matrix_factorization.distributed import (ReplicaExchange, global_rmse,
+                                                  local_shard, shard_users)
+    from matrix_factorization.engine import SGDEngine
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    dev = torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    _lib.load()
+
+    nu, ni, nnz, k, kernel, desc = WORKLOADS[args.workload]
+    t0 = time.time()
+    u, i, r = synth(nu, ni, nnz)
+    log(f"data: {nnz} ratings {nu}x{ni} in {time.time() - t0:.1f}s")
+    mu = float(np.mean(r, dtype=np.float64))
+    rs = np.random.RandomState(7)
+    P0 = rs.normal(0.0, 0.1, (nu, k)).astype(args.dtype)
+    Q0 = rs.normal(0.0, 0.1, (ni, k)).astype(args.dtype)
+
+    if world > 1:
+        bounds = shard_users(u, nu, world)
+        lu, li, lr_ = local_shard(u, i, r, bounds, rank)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        P_local = P0[lo:hi]
+    else:
+        lu, li, lr_, P_local = u, i, r, P0
+    n_local = len(lu)
+    n_users_local = P_local.shape[0]
+
+    eng = SGDEngine(lu, li, lr_, n_users_local, ni, k, kernel, args.dtype, dev,
+                    gamma=1.0 / k, min_rating=1.0, max_rating=5.0, global_mean=mu)
+    t0 = time.time()
+    nb = eng.prepare_colored()
+    t_sched = time.time() - t0
+    log(f"rank {rank}: {n_local} local ratings, {nb} colours, scheduled in {t_sched:.1f}s")
+    exch = ReplicaExchange(eng) if world > 1 else None
+
+    def reset_params():
+        eng.load_params(P=P_local, bu=np.zeros(n_users_local))
+        if exch is not None:
+            exch.bind(Q0, np.zeros(ni))
+        else:
+            eng.load_params(Q=Q0, bi=np.zeros(ni))
+
+    seed = 12345
+
+    def seq_for(ep):
+        return np.random.RandomState((seed * 1000003 + ep) & 0x7FFFFFFF).permutation(nb).astype(np.int32)
+
+    # ---------------- CPU baseline + parity on a bounded sample (rank 0, N=1)
+    cpu_baseline = None
+    parity = None
+    if world == 1 and args.cpu_sample > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # test infrastructure: checker and reported baseline only
+
+        seq0 = seq_for(0)
+        sizes = np.diff(eng.colored)[seq0]
+        m = int(np.searchsorted(np.cumsum(sizes), min(args.cpu_sample, n_local))) + 1
+        m = min(m, nb)
+        reset_params()
+        eng.epoch_colored(seq0[:m], args.lr, args.reg)
+        Pg, Qg, bug, big = eng.params_numpy()
+        order = np.concatenate([np.arange(eng.colored[b], eng.colored[b + 1])
+                                for b in seq0[:m]]).astype(np.int64)
+        S = len(order)
+        us, is_, rsmp = eng.u_host[order], eng.i_host[order], eng.r_host[order].astype(np.float64)
+        P = P0.astype(np.float64)
+        Q = Q0.astype(np.float64)
+        bu = np.zeros(nu)
+        bi = np.zeros(ni)
+        log(f"cpu oracle: {S} ratings ({m} colours), FP64, 1 thread")
+        t0 = time.perf_counter()
+        oracle.sgd_pass(us, is_, rsmp, mu, bu, bi, P, Q, kernel=kernel, gamma=1.0 / k,
+                        lr=args.lr, reg=args.reg, min_rating=1.0, max_rating=5.0)
+        t_sgd = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        sse_cpu = oracle.sse(us, is_, rsmp, mu, bu, bi, P, Q, kernel=kernel,
+                             gamma=1.0 / k, min_rating=1.0, max_rating=5.0)
+        t_sse = time.perf_counter() - t0
+        sse_gpu = oracle.sse(us, is_, rsmp, mu, bug, big, Pg, Qg, kernel=kernel,
+                             gamma=1.0 / k, min_rating=1.0, max_rating=5.0)
+        rm_c, rm_g = float(np.sqrt(sse_cpu / S)), float(np.sqrt(sse_gpu / S))
+        cpu_baseline = {
+            "value": S / (t_sgd + t_sse), "unit": "rating-updates/s", "cores": 1,
+            "kind": "port",
+            "sample": (f"first {m} of {nb} colours of epoch 1 = {S} ratings of the same "
+                       f"workload: FP64 sequential SGD sweep ({t_sgd:.1f}s) + RMSE pass "
+                       f"({t_sse:.1f}s), oracle/mf_oracle.c"),
+            "sgd_only": S / t_sgd,
+        }
+        parity = {
+            "what": "RMSE over the sample after the same partial epoch from the same "
+                    "initial state: GPU FP32 vs CPU oracle FP64",
+            "rmse_gpu": rm_g, "rmse_cpu": rm_c, "abs_diff": abs(rm_g - rm_c),
+            "max_abs_dP": float(np.max(np.abs(Pg - P))),
+            "max_abs_dQ": float(np.max(np.abs(Qg - Q))),
+        }
+        log(f"cpu {cpu_baseline['value'] / 1e6:.2f} M/s; parity |drmse|={parity['abs_diff']:.2e}")
+
+    # ---------------- warmup + timed epochs
+    reset_params()
+    stride = args.timing_stride
+    sizes = np.diff(eng.colored)
+    timed_ratings = []
+
+    def epoch(ep, timed):
+        seq = seq_for(ep)
+        if exch is not None:
+            exch.begin_epoch()
+        ms = eng.epoch_colored(seq, args.lr, args.reg,
+                               timing=stride if (timed and stride > 0) else False)
+        if exch is not None:
+            exch.end_epoch()
+        eng.sse_async(ep)
+        if ms is not None:
+            timed_ratings.append(int(sizes[seq[::stride]].sum()))
+        return ms
+
+    for ep in range(args.warmup):
+        epoch(ep, False)
+        log(f"warmup epoch {ep + 1}/{args.warmup}")
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    kernel_ms = []
+    for j in range(args.steps):
+        kernel_ms.append(epoch(args.warmup + j, True))
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    n_ep = args.warmup + args.steps
+    rmse = global_rmse(eng, n_ep, nnz)
+
+    if rank == 0:
+        value = nnz * args.steps / elapsed
+        bytes_per_update = (16 * k + 28) if args.dtype == "float32" else (32 * k + 44)
+        roofline = None
+        if stride > 0 and args.steps > 0:
+            ksum = float(sum(m[0] for m in kernel_ms)) / 1e3       # s, bracketed launches
+            launches = int(sum(m[1] for m in kernel_ms))
+            rated = int(sum(timed_ratings))
+            alg = bytes_per_update * rated                         # algorithmic bytes
+            achieved = alg / ksum / 1e9
+            traffic = traffic_from_profiles(args.workload, world)
+            roofline = {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "kernel": "k_sgd_batch",
+                "timed_launches": launches, "timing_stride": stride,
+                "avg_launch_us": ksum / launches * 1e6,
+                "alg_bytes_per_launch": alg / launches,
+                "bytes_per_update": bytes_per_update,
+                "sgd_kernel_updates_per_s": rated / ksum,
+            }
+        out = {
+            "metric": METRIC, "value": value, "unit": "rating-updates/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None,
+            "dtype": "f32" if args.dtype == "float32" else "f64",
+            "data": "synthetic",
+            "config": {"workload": desc, "n_users": nu, "n_items": ni, "nnz": nnz,
+                       "n_factors": k, "kernel": kernel, "lr": args.lr, "reg": args.reg,
+                       "schedule": f"colored ({nb} conflict-free batches/epoch on rank 0)",
+                       "parallelism": f"user-sharded dp{world}" if world > 1 else "single GPU",
+                       "step": "one epoch: SGD sweep + training-RMSE pass"},
+            "final_rmse": rmse[-1], "rmse_per_epoch": rmse,
+            "roofline": roofline, "cpu_baseline": cpu_baseline, "parity": parity,
+            "schedule_build_s": t_sched,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

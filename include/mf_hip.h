@@ -51,7 +51,9 @@ enum { MF_LINEAR = 0, MF_SIGMOID = 1, MF_RBF = 2 };
 
 /* flags for mf_sgd_epoch */
 enum {
-    MF_FLAG_XCD_SWIZZLE = 1   /* map consecutive tiles of a batch onto one XCD */
+    MF_FLAG_XCD_SWIZZLE = 1,  /* map consecutive tiles of a batch onto one XCD */
+    MF_FLAG_NT_USER = 2,      /* stream user rows/biases/triples non-temporally */
+    MF_FLAG_NT_ITEM = 4       /* store item rows/biases non-temporally          */
 };
 
 const char* mf_last_error(void);
@@ -79,8 +81,10 @@ int mf_max_factors(void);
  *   order          device, nullable: schedule position -> rating index; when
  *                  NULL, position p is rating p (ratings pre-sorted)
  *   batch_offsets  HOST, n_batches + 1 positions (non-decreasing, last <= n)
- *   batch_seq      HOST, nullable, n_batches: launch order (permutation);
- *                  NULL = 0, 1, ..., n_batches - 1
+ *   batch_seq      HOST, nullable, n_seq batch indices: launch order (a full
+ *                  epoch passes a permutation of 0..n_batches-1; a prefix
+ *                  applies a partial epoch).  NULL = 0, 1, ..., n_batches-1
+ *                  and n_seq is ignored
  *   user_biases / item_biases      device, dtype, n_users / n_items
  *   user_features / item_features  device, dtype, row-major
  *                  (n_users, n_factors) / (n_items, n_factors)
@@ -88,14 +92,17 @@ int mf_max_factors(void);
  *                  as KernelMF (a = min_rating, c = max_rating - min_rating,
  *                  kernel_matrix_factorization.py:405-406)
  *   update_user_params / update_item_params   as _sgd (:336-337)
- *   kernel_ms      host, nullable: when given, each batch launch is
- *                  bracketed by hipEvents, the stream is synchronised and the
- *                  summed kernel time (ms) is written here.
+ *   flags          MF_FLAG_* bits; bits 16..23 = timing stride S (0 = 1)
+ *   kernel_ms      host, nullable, 2 doubles: when given, every S-th launch
+ *                  is bracketed by hipEvents on `stream`, the stream is
+ *                  synchronised, kernel_ms[0] = summed time (ms) of the
+ *                  bracketed launches and kernel_ms[1] = their count.
  */
 int mf_sgd_epoch(const int32_t* user_ids, const int32_t* item_ids,
                  const void* ratings, int64_t n_ratings, const int32_t* order,
-                 const int64_t* batch_offsets, const int32_t* batch_seq,
-                 int32_t n_batches, double global_mean, void* user_biases,
+                 const int64_t* batch_offsets, int32_t n_batches,
+                 const int32_t* batch_seq, int32_t n_seq,
+                 double global_mean, void* user_biases,
                  void* item_biases, void* user_features, void* item_features,
                  int32_t n_users, int32_t n_items, int32_t n_factors,
                  int32_t kernel, int32_t dtype, double gamma, double lr,
@@ -110,6 +117,9 @@ int mf_sgd_epoch(const int32_t* user_ids, const int32_t* item_ids,
  * double *sse_out (no host sync).  `workspace` is a device buffer of at
  * least mf_sse_workspace_bytes(n_ratings) bytes.  Deterministic: the same
  * inputs give the same bits.
+ * slice_offsets (HOST, nullable, n_slices + 1 <= 17 entries): the ratings
+ * are ordered by mf_sched_slices; slice x is walked by the workgroups
+ * b % n_slices == x (XCD-local Q slices).  NULL = one slice.
  */
 size_t mf_sse_workspace_bytes(int64_t n_ratings);
 int mf_sse(const int32_t* user_ids, const int32_t* item_ids,
@@ -117,7 +127,8 @@ int mf_sse(const int32_t* user_ids, const int32_t* item_ids,
            const void* user_biases, const void* item_biases,
            const void* user_features, const void* item_features,
            int32_t n_factors, int32_t kernel, int32_t dtype, double gamma,
-           double min_rating, double max_rating, void* workspace,
+           double min_rating, double max_rating,
+           const int64_t* slice_offsets, int32_t n_slices, void* workspace,
            double* sse_out, void* stream);
 
 /*
@@ -162,7 +173,8 @@ int mf_topk(const int32_t* query_users, int32_t n_query, double global_mean,
 int mf_bias_sgd_epoch(const int32_t* user_ids, const int32_t* item_ids,
                       const void* ratings, int64_t n_ratings,
                       const int32_t* order, const int64_t* batch_offsets,
-                      const int32_t* batch_seq, int32_t n_batches,
+                      int32_t n_batches, const int32_t* batch_seq,
+                      int32_t n_seq,
                       double global_mean, void* user_biases,
                       void* item_biases, int32_t dtype, double lr, double reg,
                       int32_t update_user_params, int32_t update_item_params,
@@ -197,6 +209,20 @@ int mf_bias_predict(const int32_t* user_ids, const int32_t* item_ids,
                     const void* user_biases, const void* item_biases,
                     int32_t dtype, double min_rating, double max_rating,
                     int32_t bound_ratings, void* out, void* stream);
+
+/* ---------------- multi-GPU replica exchange ----------------------------- */
+
+/*
+ * Element-wise helper around the per-epoch all-reduce of the replicated item
+ * parameters (user-sharded data parallelism; no
+ * counterpart in the single-process reference):
+ *   mode 0 (MF_DELTA_TAKE):  cur[j] = cur[j] - base[j]   (local update delta)
+ *   mode 1 (MF_DELTA_APPLY): cur[j] = cur[j] + base[j]   (base + summed delta)
+ * cur, base: device, n values of dtype.
+ */
+enum { MF_DELTA_TAKE = 0, MF_DELTA_APPLY = 1 };
+int mf_replica_delta(void* cur, const void* base, int64_t n, int32_t dtype,
+                     int32_t mode, void* stream);
 
 /* ---------------- host-side schedulers (no GPU) -------------------------- */
 
@@ -235,6 +261,19 @@ int mf_sched_color(const int32_t* user_ids, const int32_t* item_ids,
                    int64_t n, int32_t n_users, int32_t n_items,
                    int32_t* sched_out, int64_t* color_offsets,
                    int64_t offsets_cap, int32_t* n_colors_out);
+
+/*
+ * Evaluation order for the read-only passes (mf_sse, mf_sse_sliced).  Items
+ * are cut into n_slices contiguous id ranges (n_slices = 8: one per XCD, so
+ * one slice of Q fits an XCD's 4 MiB L2); ratings are grouped by slice and,
+ * inside a slice, by user (consecutive ratings share the user's P row).
+ *   sched_out      host, n: rating indices in that order
+ *   slice_offsets  host, n_slices + 1
+ */
+int mf_sched_slices(const int32_t* user_ids, const int32_t* item_ids,
+                    int64_t n, int32_t n_users, int32_t n_items,
+                    int32_t n_slices, int32_t* sched_out,
+                    int64_t* slice_offsets);
 
 #ifdef __cplusplus
 }

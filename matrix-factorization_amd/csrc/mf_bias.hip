@@ -41,7 +41,7 @@ __global__ __launch_bounds__(kBlock) void k_bias_sse(const int32_t* __restrict__
         const T err = r[j] - pred;                                // :208
         acc += (double)err * (double)err;
     }
-    acc = group_sum<kWave>(acc);
+    acc = wave_sum(acc);
     __shared__ double red[kWavesPerBlock];
     if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = acc;
     __syncthreads();
@@ -55,7 +55,7 @@ __global__ __launch_bounds__(kBlock) void k_bias_sse(const int32_t* __restrict__
 __global__ void k_sum_partials_bias(const double* part, int n, double* out) {
     double t = 0.0;
     for (int j = threadIdx.x; j < n; j += kBlock) t += part[j];
-    t = group_sum<kWave>(t);
+    t = wave_sum(t);
     __shared__ double red[kWavesPerBlock];
     if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = t;
     __syncthreads();
@@ -132,8 +132,9 @@ using namespace mf;
 
 extern "C" int mf_bias_sgd_epoch(const int32_t* user_ids, const int32_t* item_ids,
                                  const void* ratings, int64_t n_ratings, const int32_t* order,
-                                 const int64_t* batch_offsets, const int32_t* batch_seq,
-                                 int32_t n_batches, double global_mean, void* user_biases,
+                                 const int64_t* batch_offsets, int32_t n_batches,
+                                 const int32_t* batch_seq, int32_t n_seq,
+                                 double global_mean, void* user_biases,
                                  void* item_biases, int32_t dtype, double lr, double reg,
                                  int32_t update_user_params, int32_t update_item_params,
                                  void* stream) {
@@ -143,22 +144,28 @@ extern "C" int mf_bias_sgd_epoch(const int32_t* user_ids, const int32_t* item_id
     }
     for (int32_t b = 0; b < n_batches; ++b) {
         if (batch_offsets[b] < 0 || batch_offsets[b + 1] < batch_offsets[b] ||
-            batch_offsets[b + 1] > n_ratings ||
-            (batch_seq && (batch_seq[b] < 0 || batch_seq[b] >= n_batches))) {
+            batch_offsets[b + 1] > n_ratings) {
             set_error("mf_bias_sgd_epoch: invalid batch %d", b);
             return MF_ERR_INVALID;
         }
     }
-    if (n_ratings == 0 || n_batches == 0) return MF_OK;
+    const int32_t n_launch = batch_seq ? n_seq : n_batches;
+    for (int32_t q = 0; batch_seq && q < n_seq; ++q) {
+        if (batch_seq[q] < 0 || batch_seq[q] >= n_batches) {
+            set_error("mf_bias_sgd_epoch: batch_seq[%d] out of range", q);
+            return MF_ERR_INVALID;
+        }
+    }
+    if (n_ratings == 0 || n_launch <= 0) return MF_OK;
     hipStream_t s = (hipStream_t)stream;
     const int uu = update_user_params ? 1 : 0, ui = update_item_params ? 1 : 0;
     if (dtype == MF_F32)
         return bias_sgd_run<float>(user_ids, item_ids, ratings, order, batch_offsets, batch_seq,
-                                   n_batches, global_mean, user_biases, item_biases, lr, reg, uu,
+                                   n_launch, global_mean, user_biases, item_biases, lr, reg, uu,
                                    ui, s);
     if (dtype == MF_F64)
         return bias_sgd_run<double>(user_ids, item_ids, ratings, order, batch_offsets, batch_seq,
-                                    n_batches, global_mean, user_biases, item_biases, lr, reg,
+                                    n_launch, global_mean, user_biases, item_biases, lr, reg,
                                     uu, ui, s);
     set_error("unknown dtype code %d", dtype);
     return MF_ERR_INVALID;
@@ -253,6 +260,45 @@ extern "C" int mf_bias_predict(const int32_t* user_ids, const int32_t* item_ids,
                            item_ids, n_pairs, global_mean, (const double*)user_biases,
                            (const double*)item_biases, bound_ratings ? 1 : 0, min_rating,
                            max_rating, (double*)out);
+    else {
+        set_error("unknown dtype code %d", dtype);
+        return MF_ERR_INVALID;
+    }
+    MF_HIP_CHECK(hipGetLastError());
+    return MF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Replica exchange helper (multi-GPU): cur -= base / cur += base, 16-B lanes.
+namespace mf {
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_replica_delta(T* __restrict__ cur,
+                                                          const T* __restrict__ base, int64_t n,
+                                                          int mode) {
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < n;
+         j += (int64_t)gridDim.x * kBlock) {
+        const T b = base[j];
+        cur[j] = mode == MF_DELTA_TAKE ? cur[j] - b : cur[j] + b;
+    }
+}
+}  // namespace mf
+
+extern "C" int mf_replica_delta(void* cur, const void* base, int64_t n, int32_t dtype,
+                                int32_t mode, void* stream) {
+    if (n < 0 || (n > 0 && (!cur || !base)) || (mode != MF_DELTA_TAKE && mode != MF_DELTA_APPLY)) {
+        set_error("mf_replica_delta: bad arguments");
+        return MF_ERR_INVALID;
+    }
+    if (n == 0) return MF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t need = (n + kBlock - 1) / kBlock;
+    const unsigned g = (unsigned)(need < 4096 ? need : 4096);
+    if (dtype == MF_F32)
+        hipLaunchKernelGGL(k_replica_delta<float>, dim3(g), dim3(kBlock), 0, s, (float*)cur,
+                           (const float*)base, n, mode);
+    else if (dtype == MF_F64)
+        hipLaunchKernelGGL(k_replica_delta<double>, dim3(g), dim3(kBlock), 0, s, (double*)cur,
+                           (const double*)base, n, mode);
     else {
         set_error("unknown dtype code %d", dtype);
         return MF_ERR_INVALID;

@@ -42,10 +42,79 @@ __device__ __forceinline__ int64_t xcd_swizzle(int64_t b, int64_t nb) {
     return start + w;
 }
 
+// ---- group sums on DPP (no LDS crossbar traffic) ------------------------
+// Row (16-lane) all-reduce: quad_perm xor1, quad_perm xor2, row_half_mirror,
+// row_mirror.  Each step adds two values that are uniform over the lanes
+// being combined, so every lane of a row ends with the bit-identical sum.
+// 64 lanes: + row_bcast:15 / row_bcast:31, then lane 63 is read as a scalar.
+// 32 lanes: + one xor-16 swap (ds_bpermute).
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, ROWS, 0xf, false);
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(dpp_i<CTRL, ROWS>(__float_as_int(v)));
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ double dpp(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = dpp_i<CTRL, ROWS>((int)(b & 0xffffffffLL));
+    const int hi = dpp_i<CTRL, ROWS>((int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+constexpr int kDppXor1 = 0xB1;          // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;          // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141;   // row_half_mirror
+constexpr int kDppMirror = 0x140;       // row_mirror
+constexpr int kDppBcast15 = 0x142;      // row_bcast:15
+constexpr int kDppBcast31 = 0x143;      // row_bcast:31
+
+template <typename T>
+__device__ __forceinline__ T row_sum(T v) {
+    v = v + dpp<kDppXor1>(v);
+    v = v + dpp<kDppXor2>(v);
+    v = v + dpp<kDppHalfMirror>(v);
+    v = v + dpp<kDppMirror>(v);
+    return v;
+}
+
+__device__ __forceinline__ float lane63(float v) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ double lane63(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), 63);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
 template <int GS, typename T>
 __device__ __forceinline__ T group_sum(T v) {
+    static_assert(GS == 1 || GS == 2 || GS == 4 || GS == 8 || GS == 16 || GS == 32 || GS == 64,
+                  "group of 1..64 lanes (power of two)");
+    if constexpr (GS < 16) {
+        if constexpr (GS >= 2) v = v + dpp<kDppXor1>(v);
+        if constexpr (GS >= 4) v = v + dpp<kDppXor2>(v);
+        if constexpr (GS >= 8) v = v + dpp<kDppHalfMirror>(v);
+        return v;
+    }
+    v = row_sum(v);
+    if constexpr (GS == 32) {
+        v = v + __shfl_xor(v, 16, kWave);
+    } else if constexpr (GS == 64) {
+        v = v + dpp<kDppBcast15, 0xa>(v);      // rows 1, 3 += rows 0, 2
+        v = v + dpp<kDppBcast31, 0xc>(v);      // rows 2, 3 += rows 0 + 1
+        v = lane63(v);                         // (R3 + R2) + (R1 + R0), uniform
+    }
+    return v;
+}
+
+// Whole-wave sum for integer/FP64 partials (block reductions; not hot).
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll
-    for (int o = 1; o < GS; o <<= 1) v = v + __shfl_xor(v, o, kWave);
+    for (int o = 1; o < kWave; o <<= 1) v = v + __shfl_xor(v, o, kWave);
     return v;
 }
 
@@ -72,6 +141,12 @@ __device__ __forceinline__ double rl_f(double v, int src) {
     const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+
+// W consecutive values of a row moved by one lane (16 B for float4/double2)
+template <typename T, int W> struct VecOf;
+template <typename T> struct VecOf<T, 1> { using type = T; };
+template <typename T> struct VecOf<T, 2> { typedef T type __attribute__((ext_vector_type(2))); };
+template <typename T> struct VecOf<T, 4> { typedef T type __attribute__((ext_vector_type(4))); };
 
 template <typename T> __device__ __forceinline__ T dexp(T x);
 template <> __device__ __forceinline__ float dexp<float>(float x) { return expf(x); }

@@ -1,0 +1,561 @@
+// mf_rows.hpp -- the two hot kernels of the KernelMF path and their launchers:
+//   k_sgd_batch  one conflict-free batch of SGD updates (kernels.py:108-327
+//                applied to every rating of the batch)
+//   k_sse_stream training sum of squared errors (_calculate_rmse,
+//                kernel_matrix_factorization.py:240-317)
+//
+// Row layout.  A factor row of k values is moved by a
+// GROUP of GS lanes; each lane moves W consecutive values per access (W = 4
+// for float, 2 for double when k allows: one 16-B global_load_dwordx4 per
+// lane), V accesses per lane.  GS <= 16 for W > 1, so a group is (part of) a
+// DPP row and the dot product reduces with 0..4 DPP adds; R = 64 / GS
+// ratings share one wave instruction.  W = 1 keeps 16/32/64-lane groups for
+// k that is not a multiple of W.
+//
+// Included by mf_rows_f32.hip / mf_rows_f64.hip (one dtype each).
+#pragma once
+
+#include <algorithm>
+#include <vector>
+
+#include "mf_common.hpp"
+
+namespace mf {
+
+// ------------------------------------------------------------ memory ops
+// User rows, user biases and triples stream through once per batch: load and
+// store them non-temporally so they do not evict item rows from L2.
+template <bool NT, typename X>
+__device__ __forceinline__ X ld(const X* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT, typename X>
+__device__ __forceinline__ void st(X* p, X v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <typename T>
+struct SgdArgs {
+    const int32_t* u;
+    const int32_t* i;
+    const T* r;
+    const int32_t* order;   // nullable: position -> rating index
+    T* P;
+    T* Q;
+    T* Bu;
+    T* Bi;
+    int64_t off;            // first schedule position of this batch
+    int64_t n;              // ratings in this batch
+    int32_t k;
+    int32_t upd_user;
+    int32_t upd_item;
+    int32_t swizzle;
+    Hyper<T> h;
+};
+
+template <typename T>
+struct ReadArgs {
+    const int32_t* u;
+    const int32_t* i;
+    const T* r;
+    const T* P;
+    const T* Q;
+    const T* Bu;
+    const T* Bi;
+    int64_t n;
+    int32_t k;
+    int32_t bound;
+    T* out;
+    double* partials;
+    Hyper<T> h;
+};
+
+// Work split of the read-only passes: `n` slices of the rating array (the
+// item-range slices of mf_sched_slices), slice x walked by the workgroups
+// b with b % n == x.  Placement only changes speed.
+constexpr int kMaxSlices = 16;
+struct SliceTab {
+    int64_t off[kMaxSlices + 1];
+    int32_t n;
+};
+
+// kernels.py:21-105.  `s` = group-reduced dot product (linear/sigmoid) or
+// squared distance (rbf).
+template <typename T, int KERN>
+__device__ __forceinline__ T predict_one(T s, T bu, T bi, const Hyper<T>& h) {
+    if constexpr (KERN == MF_LINEAR) {
+        return ((h.mu + bi) + bu) + s;                       // kernels.py:42-44
+    } else if constexpr (KERN == MF_SIGMOID) {
+        const T lin = ((h.mu + bu) + bi) + s;                // kernels.py:73-75
+        const T sg = (T)1 / ((T)1 + dexp<T>(-lin));          // kernels.py:17
+        return h.a + h.c * sg;                               // kernels.py:77
+    } else {
+        return h.a + h.c * dexp<T>((-h.gamma) * s);          // kernels.py:102-104
+    }
+}
+
+// rating-slot broadcast: wave-uniform source -> v_readlane, else ds_bpermute
+template <int GS>
+__device__ __forceinline__ int take_i(int v, int src) {
+    if constexpr (GS == kWave) return rl_i32(v, src);
+    else return bcast_i32(v, src);
+}
+template <int GS, typename T>
+__device__ __forceinline__ T take_f(T v, int src) {
+    if constexpr (GS == kWave) return rl_f(v, src);
+    else return bcast_f(v, src);
+}
+
+// Rating slots per wave: ~16 ratings and <= 32 row registers per operand.
+template <int R, int V, int W>
+struct SlotsFor {
+    static constexpr int a = 16 / R > 0 ? 16 / R : 1;
+    static constexpr int b = 32 / (V * W) > 0 ? 32 / (V * W) : 1;
+    static constexpr int c = a < b ? a : b;
+    static constexpr int S = c > 8 ? 8 : c;
+};
+
+// Gather the rows of S rating slots: all loads issued before any use;
+// indices clamped so no load sits behind a branch; vector slots past the
+// row end are zeroed afterwards.
+template <typename T, int W, int GS, int V, int S, bool NT>
+__device__ __forceinline__ void gather_rows(const T* base, const int (&id)[S], int k, int kv, int l,
+                                            typename VecOf<T, W>::type (&out)[S][V]) {
+    using VT = typename VecOf<T, W>::type;
+#pragma unroll
+    for (int x = 0; x < S; ++x) {
+        const VT* row = reinterpret_cast<const VT*>(base + (int64_t)id[x] * k);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const int vi = v * GS + l;
+            out[x][v] = ld<NT>(row + (vi < kv ? vi : kv - 1));
+        }
+    }
+#pragma unroll
+    for (int x = 0; x < S; ++x)
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+            if (v * GS + l >= kv) out[x][v] = (VT)(T)0;
+}
+
+template <typename T, int W, int V, int KERN>
+__device__ __forceinline__ T lane_partial(const typename VecOf<T, W>::type (&p)[V],
+                                          const typename VecOf<T, W>::type (&q)[V]) {
+    T s = (T)0;
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            T a, b;
+            if constexpr (W == 1) { a = p[v]; b = q[v]; }
+            else { a = p[v][w]; b = q[v][w]; }
+            if constexpr (KERN == MF_RBF) {
+                const T d = a - b;
+                s = s + d * d;
+            } else {
+                s = s + a * b;
+            }
+        }
+    }
+    return s;
+}
+
+// ------------------------------------------------------------- SGD batch
+// Wave w applies ratings [w*RPW, (w+1)*RPW) of the batch (RPW = S*R):
+//   1. lane j loads triple j and gathers b_u / b_i of rating j;
+//   2. all rows of all slots are loaded;
+//   3. per slot: dot product (DPP), update, predicated stores.
+// No two ratings of a batch share a row, so no slot reads another's write.
+template <typename T, int W, int GS, int V, int KERN, int S, bool NT>
+__global__ __launch_bounds__(kBlock) void k_sgd_batch(SgdArgs<T> A) {
+    using VT = typename VecOf<T, W>::type;
+    constexpr int R = kWave / GS;
+    constexpr int RPW = S * R;
+    static_assert(RPW <= kWave, "one lane per rating for the triple loads");
+
+    const int lane = threadIdx.x & (kWave - 1);
+    const int g = lane / GS;
+    const int l = lane % GS;
+    const int64_t blk = A.swizzle ? xcd_swizzle(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t w0 = (blk * kWavesPerBlock + threadIdx.x / kWave) * RPW;
+    if (w0 >= A.n) return;
+    const int nw = (int)min((int64_t)RPW, A.n - w0);
+    const int k = A.k;
+    const int kv = k / W;
+    const Hyper<T> h = A.h;
+
+    int tu, ti;
+    T tr, tbu = (T)0, tbi = (T)0;
+    {
+        const int64_t pos = A.off + w0 + (lane < nw ? lane : 0);
+        const int64_t j = A.order ? (int64_t)A.order[pos] : pos;
+        tu = ld<NT>(A.u + j);
+        ti = ld<NT>(A.i + j);
+        tr = ld<NT>(A.r + j);
+        if constexpr (KERN != MF_RBF) {
+            tbu = ld<NT>(A.Bu + tu);
+            tbi = A.Bi[ti];
+        }
+    }
+
+    int uu[S], ii[S];
+    bool have[S];
+    T rr[S];
+#pragma unroll
+    for (int x = 0; x < S; ++x) {
+        const int idx = x * R + g;
+        have[x] = idx < nw;
+        const int src = have[x] ? idx : 0;
+        uu[x] = take_i<GS>(tu, src);
+        ii[x] = take_i<GS>(ti, src);
+        rr[x] = take_f<GS>(tr, src);
+    }
+    VT p[S][V], q[S][V];
+    if (kv > 0) {
+        gather_rows<T, W, GS, V, S, NT>(A.P, uu, k, kv, l, p);
+        gather_rows<T, W, GS, V, S, false>(A.Q, ii, k, kv, l, q);
+    } else {
+#pragma unroll
+        for (int x = 0; x < S; ++x)
+#pragma unroll
+            for (int v = 0; v < V; ++v) p[x][v] = q[x][v] = (VT)(T)0;
+    }
+    T bu[S], bi[S];
+#pragma unroll
+    for (int x = 0; x < S; ++x) {             // overlaps the row loads in flight
+        const int src = have[x] ? x * R + g : 0;
+        bu[x] = KERN != MF_RBF ? take_f<GS>(tbu, src) : (T)0;
+        bi[x] = KERN != MF_RBF ? take_f<GS>(tbi, src) : (T)0;
+    }
+
+#pragma unroll
+    for (int x = 0; x < S; ++x) {
+        const T s = group_sum<GS>(lane_partial<T, W, V, KERN>(p[x], q[x]));
+        T e, d = (T)1;
+        if constexpr (KERN == MF_LINEAR) {
+            const T pred = ((h.mu + bi[x]) + bu[x]) + s;             // kernels.py:148-153
+            e = pred - rr[x];                                        // :156
+        } else if constexpr (KERN == MF_SIGMOID) {
+            const T lin = ((h.mu + bu[x]) + bi[x]) + s;              // kernels.py:226-228
+            const T ex = dexp<T>(-lin);
+            const T sg = (T)1 / ((T)1 + ex);                         // :229
+            const T pred = h.a + h.c * sg;                           // :230
+            e = pred - rr[x];                                        // :233
+            d = (sg * sg) * ex;                                      // :236 (no c factor)
+        } else {
+            const T E = dexp<T>((-h.gamma) * s);                     // kernels.py:302-303
+            const T pred = h.a + h.c * E;                            // :304
+            e = pred - rr[x];                                        // :307
+            d = ((T)2 * E) * h.gamma;                                // :310 (no c factor)
+        }
+        const bool lead = have[x] && l == 0;
+        if constexpr (KERN == MF_LINEAR) {                           // kernels.py:159-163
+            if (A.upd_user && lead) st<NT>(A.Bu + uu[x], bu[x] - h.lr * (e + h.reg * bu[x]));
+            if (A.upd_item && lead) A.Bi[ii[x]] = bi[x] - h.lr * (e + h.reg * bi[x]);
+        } else if constexpr (KERN == MF_SIGMOID) {                   // kernels.py:239-245
+            if (A.upd_user && lead) st<NT>(A.Bu + uu[x], bu[x] - h.lr * (e * d + h.reg * bu[x]));
+            if (A.upd_item && lead) A.Bi[ii[x]] = bi[x] - h.lr * (e * d + h.reg * bi[x]);
+        }
+        VT* pw = reinterpret_cast<VT*>(A.P + (int64_t)uu[x] * k);
+        VT* qw = reinterpret_cast<VT*>(A.Q + (int64_t)ii[x] * k);
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const int vi = v * GS + l;
+            if (!(have[x] && vi < kv)) continue;
+            const VT pf = p[x][v], qf = q[x][v];
+            VT np, nq;
+            if constexpr (KERN == MF_LINEAR) {                       // kernels.py:166-178
+                np = pf - h.lr * (e * qf + h.reg * pf);
+                nq = qf - h.lr * (e * pf + h.reg * qf);
+            } else if constexpr (KERN == MF_SIGMOID) {               // kernels.py:248-260
+                np = pf - h.lr * (e * (qf * d) + h.reg * pf);
+                nq = qf - h.lr * (e * (pf * d) + h.reg * qf);
+            } else {                                                 // kernels.py:313-325
+                np = pf - h.lr * (e * (d * (qf - pf)) + h.reg * pf);
+                nq = qf - h.lr * (e * (d * (pf - qf)) + h.reg * qf);
+            }
+            if (A.upd_user) st<NT>(pw + vi, np);
+            if (A.upd_item) qw[vi] = nq;
+        }
+    }
+}
+
+// -------------------------------------------------------- training SSE
+// Each wave owns a contiguous run of its slice; triples arrive 64 at a time
+// (lane j <-> rating j) and the next chunk's triples are in flight while the
+// current chunk is consumed S*R ratings per step.  In mf_sched_slices order
+// consecutive ratings share the user's P row and a slice's Q rows stay in one
+// XCD's L2.
+template <typename T, int W, int GS, int V, int KERN, int S>
+__global__ __launch_bounds__(kBlock) void k_sse_stream(ReadArgs<T> A, SliceTab SL) {
+    using VT = typename VecOf<T, W>::type;
+    constexpr int R = kWave / GS;
+    constexpr int STEP = S * R;
+    static_assert(kWave % STEP == 0, "chunk of 64 ratings = whole steps");
+    const int lane = threadIdx.x & (kWave - 1);
+    const int g = lane / GS;
+    const int l = lane % GS;
+    const int k = A.k;
+    const int kv = k / W;
+    const Hyper<T> h = A.h;
+    const int x_slice = blockIdx.x % SL.n;
+    const int64_t bps = gridDim.x / SL.n;
+    const int64_t nw_slice = bps * kWavesPerBlock;
+    const int64_t wv = (int64_t)(blockIdx.x / SL.n) * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t s0 = SL.off[x_slice], len = SL.off[x_slice + 1] - s0;
+    const int64_t b0 = s0 + len * wv / nw_slice;
+    const int64_t b1 = s0 + len * (wv + 1) / nw_slice;
+    double acc = 0.0;
+    if (b0 < b1) {
+        auto fetch = [&](int64_t c0, int& u, int& i, T& r) {
+            const int64_t j = min(c0 + lane, b1 - 1);
+            u = A.u[j]; i = A.i[j]; r = A.r[j];
+        };
+        int nu_, ni_;
+        T nr_;
+        fetch(b0, nu_, ni_, nr_);
+        for (int64_t c0 = b0; c0 < b1; c0 += kWave) {
+            const int tu = nu_, ti = ni_;
+            const T tr = nr_;
+            T tbu = (T)0, tbi = (T)0;
+            if constexpr (KERN != MF_RBF) { tbu = A.Bu[tu]; tbi = A.Bi[ti]; }
+            const int nw = (int)min((int64_t)kWave, b1 - c0);
+            if (c0 + kWave < b1) fetch(c0 + kWave, nu_, ni_, nr_);   // prefetch
+            for (int t = 0; t < nw; t += STEP) {
+                int uu[S], ii[S];
+                bool have[S];
+                T rr[S], bu[S], bi[S];
+                VT p[S][V], q[S][V];
+#pragma unroll
+                for (int x = 0; x < S; ++x) {
+                    const int idx = t + x * R + g;
+                    have[x] = idx < nw;
+                    const int src = have[x] ? idx : t;
+                    uu[x] = take_i<GS>(tu, src);
+                    ii[x] = take_i<GS>(ti, src);
+                    rr[x] = take_f<GS>(tr, src);
+                }
+                if (kv > 0) {
+                    gather_rows<T, W, GS, V, S, false>(A.P, uu, k, kv, l, p);
+                    gather_rows<T, W, GS, V, S, false>(A.Q, ii, k, kv, l, q);
+                } else {
+#pragma unroll
+                    for (int x = 0; x < S; ++x)
+#pragma unroll
+                        for (int v = 0; v < V; ++v) p[x][v] = q[x][v] = (VT)(T)0;
+                }
+#pragma unroll
+                for (int x = 0; x < S; ++x) {
+                    const int src = have[x] ? t + x * R + g : t;
+                    bu[x] = take_f<GS>(tbu, src);
+                    bi[x] = take_f<GS>(tbi, src);
+                }
+#pragma unroll
+                for (int x = 0; x < S; ++x) {
+                    const T sm = group_sum<GS>(lane_partial<T, W, V, KERN>(p[x], q[x]));
+                    const T err = rr[x] - predict_one<T, KERN>(sm, bu[x], bi[x], h);   // :313
+                    if (have[x] && l == 0) acc += (double)err * (double)err;
+                }
+            }
+        }
+    }
+    acc = wave_sum(acc);
+    __shared__ double red[kWavesPerBlock];
+    if (lane == 0) red[threadIdx.x / kWave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; ++w) t += red[w];
+        A.partials[blockIdx.x] = t;
+    }
+}
+
+__global__ void k_sum_partials(const double* part, int n, double* out);
+
+constexpr int kSseMaxBlocks = 2048;
+
+// ------------------------------------------------ (dtype, k) -> row layout
+// Calls F.template run<W, GS, V, KERN>() for dtype T.
+template <typename T, typename F>
+int dispatch_rows(int k, int kernel, F&& f) {
+    constexpr int WV = 16 / (int)sizeof(T);           // values per 16-B access
+    if (k < 0 || k > kMaxFactors) {
+        set_error("n_factors=%d outside [0, %d]", k, kMaxFactors);
+        return MF_ERR_INVALID;
+    }
+    if (kernel < MF_LINEAR || kernel > MF_RBF) {
+        set_error("unknown kernel code %d", kernel);
+        return MF_ERR_INVALID;
+    }
+#define MF_K3(W, GS, V)                                                         \
+    {                                                                           \
+        if (kernel == MF_LINEAR) return f.template run<W, GS, V, MF_LINEAR>();  \
+        if (kernel == MF_SIGMOID) return f.template run<W, GS, V, MF_SIGMOID>();\
+        return f.template run<W, GS, V, MF_RBF>();                              \
+    }
+    if (k > 0 && k % WV == 0 && k / WV <= 256) {
+        int kvp = 1;
+        while (kvp < k / WV) kvp <<= 1;
+        switch (kvp) {
+            case 1: MF_K3(WV, 1, 1)
+            case 2: MF_K3(WV, 2, 1)
+            case 4: MF_K3(WV, 4, 1)
+            case 8: MF_K3(WV, 8, 1)
+            case 16: MF_K3(WV, 16, 1)
+            case 32: MF_K3(WV, 16, 2)
+            case 64: MF_K3(WV, 16, 4)
+            case 128: MF_K3(WV, 16, 8)
+            case 256: MF_K3(WV, 16, 16)
+            default: break;
+        }
+    } else {
+        switch (kpad_of(k)) {
+            case 16: MF_K3(1, 16, 1)
+            case 32: MF_K3(1, 32, 1)
+            case 64: MF_K3(1, 64, 1)
+            case 128: MF_K3(1, 64, 2)
+            case 256: MF_K3(1, 64, 4)
+            case 512: MF_K3(1, 64, 8)
+            case 1024: MF_K3(1, 64, 16)
+            default: break;
+        }
+    }
+#undef MF_K3
+    set_error("internal: no row layout for n_factors=%d", k);
+    return MF_ERR_INVALID;
+}
+
+// ----------------------------------------------------------- launchers
+struct SgdParams {
+    const int32_t* u; const int32_t* i; const void* r; const int32_t* order;
+    const int64_t* offs; const int32_t* seq; int32_t nl;     // nl = launches
+    double mu; void* bu; void* bi; void* P; void* Q; int32_t k; int32_t kernel;
+    double gamma, lr, reg, lo, hi; int32_t uu, ui, flags;
+    hipStream_t stream; double* kernel_ms;
+};
+
+struct SseParams {
+    const int32_t* u; const int32_t* i; const void* r; int64_t n;
+    double mu; const void* bu; const void* bi; const void* P; const void* Q;
+    int32_t k; int32_t kernel; double gamma, lo, hi;
+    double* partials; double* sse_out; hipStream_t stream; SliceTab S;
+};
+
+template <typename T>
+struct SgdRun {
+    const SgdParams& p;
+
+    // flags bits 8..11: experimental slot count for the rank-64 FP32 layout
+    template <int W, int GS, int V, int KERN>
+    int run() {
+        constexpr int SD = SlotsFor<kWave / GS, V, W>::S;
+        if constexpr (std::is_same<T, float>::value && W == 4 && GS == 16 && V == 1) {
+            switch ((p.flags >> 8) & 0xf) {
+                case 1: return go<W, GS, V, KERN, 2>();
+                case 2: return go<W, GS, V, KERN, 8>();
+                case 3: return go<W, GS, V, KERN, 1>();
+                default: break;
+            }
+        }
+        return go<W, GS, V, KERN, SD>();
+    }
+
+    template <int W, int GS, int V, int KERN, int S>
+    int go() {
+        constexpr int RPW = S * (kWave / GS);
+        SgdArgs<T> a;
+        a.u = p.u; a.i = p.i; a.r = static_cast<const T*>(p.r); a.order = p.order;
+        a.P = static_cast<T*>(p.P); a.Q = static_cast<T*>(p.Q);
+        a.Bu = static_cast<T*>(p.bu); a.Bi = static_cast<T*>(p.bi);
+        a.k = p.k; a.upd_user = p.uu; a.upd_item = p.ui;
+        a.swizzle = (p.flags & MF_FLAG_XCD_SWIZZLE) ? 1 : 0;
+        a.h = make_hyper<T>(p.mu, p.lr, p.reg, p.gamma, p.lo, p.hi);
+        const bool nt = (p.flags & MF_FLAG_NT_USER) != 0;
+        // optional timing: hipEvents around every `stride`-th launch
+        const int stride = std::max(1, (p.flags >> 16) & 0xff);
+        std::vector<hipEvent_t> ev;
+        if (p.kernel_ms) {
+            ev.resize(2 * (size_t)((p.nl + stride - 1) / stride));
+            for (auto& e : ev) MF_HIP_CHECK(hipEventCreate(&e));
+        }
+        int rc = MF_OK;
+        int32_t timed = 0;
+        for (int32_t s = 0; s < p.nl; ++s) {
+            const int32_t b = p.seq ? p.seq[s] : s;
+            a.off = p.offs[b];
+            a.n = p.offs[b + 1] - p.offs[b];
+            if (a.n <= 0) continue;
+            const int64_t waves = (a.n + RPW - 1) / RPW;
+            const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
+            const bool tm = p.kernel_ms && (s % stride == 0);
+            if (tm) {
+                hipError_t e = hipEventRecord(ev[2 * (s / stride)], p.stream);
+                if (e != hipSuccess) { rc = hip_fail(e, "hipEventRecord"); break; }
+            }
+            if (nt) hipLaunchKernelGGL((k_sgd_batch<T, W, GS, V, KERN, S, true>), grid,
+                                       dim3(kBlock), 0, p.stream, a);
+            else hipLaunchKernelGGL((k_sgd_batch<T, W, GS, V, KERN, S, false>), grid,
+                                    dim3(kBlock), 0, p.stream, a);
+            if (tm) {
+                hipError_t e = hipEventRecord(ev[2 * (s / stride) + 1], p.stream);
+                if (e != hipSuccess) { rc = hip_fail(e, "hipEventRecord"); break; }
+                ++timed;
+            }
+        }
+        hipError_t le = hipGetLastError();
+        if (rc == MF_OK && le != hipSuccess) rc = hip_fail(le, "k_sgd_batch launch");
+        if (p.kernel_ms) {
+            double tot = 0.0;
+            if (rc == MF_OK) {
+                hipError_t e = hipStreamSynchronize(p.stream);
+                if (e != hipSuccess) rc = hip_fail(e, "hipStreamSynchronize");
+            }
+            for (int32_t s = 0; rc == MF_OK && s < p.nl; s += stride) {
+                const int32_t b = p.seq ? p.seq[s] : s;
+                if (p.offs[b + 1] - p.offs[b] <= 0) continue;
+                float ms = 0.f;
+                hipError_t e = hipEventElapsedTime(&ms, ev[2 * (s / stride)],
+                                                   ev[2 * (s / stride) + 1]);
+                if (e != hipSuccess) { rc = hip_fail(e, "hipEventElapsedTime"); break; }
+                tot += ms;
+            }
+            for (auto& e : ev) (void)hipEventDestroy(e);
+            if (rc == MF_OK) { p.kernel_ms[0] = tot; p.kernel_ms[1] = (double)timed; }
+        }
+        return rc;
+    }
+};
+
+template <typename T>
+struct SseRun {
+    const SseParams& p;
+
+    template <int W, int GS, int V, int KERN>
+    int run() {
+        constexpr int S = SlotsFor<kWave / GS, V, W>::S;
+        ReadArgs<T> a;
+        a.u = p.u; a.i = p.i; a.r = static_cast<const T*>(p.r);
+        a.P = static_cast<const T*>(p.P); a.Q = static_cast<const T*>(p.Q);
+        a.Bu = static_cast<const T*>(p.bu); a.Bi = static_cast<const T*>(p.bi);
+        a.n = p.n; a.k = p.k; a.bound = 0; a.out = nullptr; a.partials = p.partials;
+        a.h = make_hyper<T>(p.mu, 0.0, 0.0, p.gamma, p.lo, p.hi);
+        const int blocks = (kSseMaxBlocks / p.S.n) * p.S.n;
+        hipLaunchKernelGGL((k_sse_stream<T, W, GS, V, KERN, S>), dim3(blocks), dim3(kBlock), 0,
+                           p.stream, a, p.S);
+        hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(kBlock), 0, p.stream,
+                           (const double*)p.partials, blocks, p.sse_out);
+        MF_HIP_CHECK(hipGetLastError());
+        return MF_OK;
+    }
+};
+
+// defined in mf_rows_f32.hip / mf_rows_f64.hip
+int sgd_launch_f32(const SgdParams& p);
+int sgd_launch_f64(const SgdParams& p);
+int sse_launch_f32(const SseParams& p);
+int sse_launch_f64(const SseParams& p);
+
+}  // namespace mf

@@ -199,3 +199,34 @@ extern "C" int mf_sched_color(const int32_t* user_ids, const int32_t* item_ids, 
     }
     return MF_OK;
 }
+
+extern "C" int mf_sched_slices(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
+                               int32_t n_users, int32_t n_items, int32_t n_slices,
+                               int32_t* sched_out, int64_t* slice_offsets) {
+    if (n < 0 || n_users < 0 || n_items < 0 || n_slices < 1 || n_slices > 64 ||
+        (n > 0 && !sched_out) || !slice_offsets) {
+        set_error("mf_sched_slices: bad arguments");
+        return MF_ERR_INVALID;
+    }
+    if (int rc = check_ids(user_ids, item_ids, n, n_users, n_items)) return rc;
+    try {
+        // stable counting sort by key = slice(item) * n_users + user
+        const int64_t nkeys = (int64_t)n_slices * n_users;
+        std::vector<int64_t> cnt((size_t)nkeys + 1, 0);
+        auto slice_of = [&](int32_t it) {
+            return (int64_t)((int64_t)it * n_slices / (n_items > 0 ? n_items : 1));
+        };
+        for (int64_t j = 0; j < n; ++j)
+            cnt[slice_of(item_ids[j]) * n_users + user_ids[j] + 1] += 1;
+        for (int64_t q = 0; q < nkeys; ++q) cnt[q + 1] += cnt[q];
+        for (int32_t x = 0; x <= n_slices; ++x) slice_offsets[x] = cnt[(int64_t)x * n_users];
+        for (int64_t j = 0; j < n; ++j) {
+            const int64_t key = slice_of(item_ids[j]) * n_users + user_ids[j];
+            sched_out[cnt[key]++] = (int32_t)j;
+        }
+    } catch (const std::bad_alloc&) {
+        set_error("mf_sched_slices: out of host memory");
+        return MF_ERR_NOMEM;
+    }
+    return MF_OK;
+}

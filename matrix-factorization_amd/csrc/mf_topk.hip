@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_select(const uint64_t* __restri
     // candidates
     int c = 0;
     for (int i = tid; i < n_items; i += kBlock) c += K[i] != 0ull;
-    c = group_sum<kWave>(c);
+    c = wave_sum(c);
     if ((tid & 63) == 0) wsum[tid / kWave] = c;
     __syncthreads();
     if (tid == 0) {

@@ -17,14 +17,17 @@ LIB_PATH = os.environ.get("MF_HIP_LIB", os.path.join(_HERE, "libmf_hip.so"))
 MF_F32, MF_F64 = 0, 1
 MF_LINEAR, MF_SIGMOID, MF_RBF = 0, 1, 2
 MF_FLAG_XCD_SWIZZLE = 1
+MF_FLAG_NT_USER = 2
+MF_FLAG_NT_ITEM = 4
 MF_ERR_CAPACITY = 3
+MF_DELTA_TAKE, MF_DELTA_APPLY = 0, 1
 KERNEL_CODES = {"linear": MF_LINEAR, "sigmoid": MF_SIGMOID, "rbf": MF_RBF}
 
 _P = ctypes.c_void_p
 _I32 = ctypes.c_int32
 _I64 = ctypes.c_int64
 _F64 = ctypes.c_double
-_PD = ctypes.POINTER(ctypes.c_double)
+_PD = ctypes.c_void_p          # double[2] timing output (nullable)
 
 # name -> (restype, argtypes); mirrors include/mf_hip.h one to one
 SIGNATURES = {
@@ -32,7 +35,7 @@ SIGNATURES = {
     "mf_abi_version": (ctypes.c_int, []),
     "mf_max_factors": (ctypes.c_int, []),
     "mf_sgd_epoch": (ctypes.c_int, [
-        _P, _P, _P, _I64, _P, _P, _P, _I32,          # ids, ratings, n, order, offs, seq, nb
+        _P, _P, _P, _I64, _P, _P, _I32, _P, _I32,    # ids, ratings, n, order, offs, nb, seq, nseq
         _F64, _P, _P, _P, _P,                         # mu, bu, bi, P, Q
         _I32, _I32, _I32,                             # n_users, n_items, k
         _I32, _I32, _F64, _F64, _F64, _F64, _F64,     # kernel dtype gamma lr reg min max
@@ -40,7 +43,7 @@ SIGNATURES = {
     "mf_sse_workspace_bytes": (ctypes.c_size_t, [_I64]),
     "mf_sse": (ctypes.c_int, [
         _P, _P, _P, _I64, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _F64, _F64,
-        _F64, _P, _P, _P]),
+        _F64, _P, _I32, _P, _P, _P]),
     "mf_predict": (ctypes.c_int, [
         _P, _P, _I64, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _F64, _F64,
         _F64, _I32, _P, _P]),
@@ -49,7 +52,7 @@ SIGNATURES = {
         _P, _I32, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _F64, _F64,
         _F64, _P, _I32, _P, _P, _P, _P]),
     "mf_bias_sgd_epoch": (ctypes.c_int, [
-        _P, _P, _P, _I64, _P, _P, _P, _I32, _F64, _P, _P, _I32, _F64, _F64,
+        _P, _P, _P, _I64, _P, _P, _I32, _P, _I32, _F64, _P, _P, _I32, _F64, _F64,
         _I32, _I32, _P]),
     "mf_bias_sse": (ctypes.c_int, [
         _P, _P, _P, _I64, _F64, _P, _P, _I32, _P, _P, _P]),
@@ -57,10 +60,12 @@ SIGNATURES = {
         _P, _P, _P, _F64, _P, _P, _I32, _I32, _P, _P, _P, _P, _I32, _F64, _P]),
     "mf_bias_predict": (ctypes.c_int, [
         _P, _P, _I64, _F64, _P, _P, _I32, _F64, _F64, _I32, _P, _P]),
+    "mf_replica_delta": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P]),
     "mf_sched_levels": (ctypes.c_int, [
         _P, _P, _I64, _P, _I32, _I32, _I32, _I32, _P, _P, _I64, _P]),
     "mf_sched_color": (ctypes.c_int, [
         _P, _P, _I64, _I32, _I32, _P, _P, _I64, _P]),
+    "mf_sched_slices": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P, _P]),
 }
 
 

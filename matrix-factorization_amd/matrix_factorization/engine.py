@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 from typing import Optional, Sequence, Tuple
 
 import numpy as np
@@ -112,6 +113,31 @@ def sched_color(u: np.ndarray, i: np.ndarray, n_users: int,
     return sched, offs[: nc.value + 1].copy()
 
 
+def sched_slices(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int,
+                 n_slices: int = 8) -> Tuple[np.ndarray, np.ndarray]:
+    """Evaluation order: rating indices grouped by item slice, then user."""
+    n = len(u)
+    u = np.ascontiguousarray(u, np.int32)
+    i = np.ascontiguousarray(i, np.int32)
+    sched = np.empty(n, np.int32)
+    offs = np.empty(n_slices + 1, np.int64)
+    _lib.call("mf_sched_slices", _np(u), _np(i), n, n_users, n_items, n_slices,
+              _np(sched), _np(offs))
+    return sched, offs
+
+
+N_SLICES = 8          # one item slice per XCD (MI355X: 8 XCDs x 4 MiB L2)
+
+
+def default_sgd_flags() -> int:
+    env = os.environ.get("MF_SGD_FLAGS")
+    if env is not None:
+        return int(env, 0)
+    # measured on MI355X (tools/sweep_sgd.py): streaming the user rows
+    # non-temporally keeps Q's XCD-local slice in L2 (-6% SGD time)
+    return _lib.MF_FLAG_XCD_SWIZZLE | _lib.MF_FLAG_NT_USER
+
+
 # --------------------------------------------------------------- engine
 class SGDEngine:
     """Ratings + factor-model parameters on one GPU.
@@ -151,6 +177,7 @@ class SGDEngine:
                        or self.i_host.min() < 0 or self.i_host.max() >= n_items):
             raise ValueError("rating ids outside [0, n_users) x [0, n_items)")
         self._upload_triples(self.u_host, self.i_host, self.r_host)
+        self._build_eval()
         self.colored = None          # (offsets,) once prepare_colored() ran
         ws = max(_lib.load().mf_sse_workspace_bytes(self.n), 8)
         self.ws = torch.empty((ws + 7) // 8, dtype=torch.float64, device=self.dev)
@@ -166,6 +193,19 @@ class SGDEngine:
         self.u = torch.from_numpy(u).to(self.dev)
         self.i = torch.from_numpy(i).to(self.dev)
         self.r = torch.from_numpy(r).to(self.dev)
+
+    def _build_eval(self):
+        """Second copy of the ratings in evaluation order (mf_sched_slices):
+        the training-RMSE pass walks one item slice per XCD, user by user."""
+        if self.bias_only or self.n == 0:
+            self.eu, self.ei, self.er, self.eval_offs = self.u, self.i, self.r, None
+            return
+        sched, offs = sched_slices(self.u_host, self.i_host, self.n_users, self.n_items,
+                                   N_SLICES)
+        self.eu = torch.from_numpy(self.u_host[sched]).to(self.dev)
+        self.ei = torch.from_numpy(self.i_host[sched]).to(self.dev)
+        self.er = torch.from_numpy(self.r_host[sched]).to(self.dev)
+        self.eval_offs = offs
 
     def _dev(self, a, shape) -> torch.Tensor:
         if isinstance(a, torch.Tensor):
@@ -215,8 +255,9 @@ class SGDEngine:
 
     def epoch_exact(self, order: np.ndarray, lr: float, reg: float,
                     update_user: bool = True, update_item: bool = True,
-                    timing: bool = False) -> Optional[float]:
-        """One epoch in the given visit order (rating indices)."""
+                    timing=False):
+        """One epoch in the given visit order (rating indices).  ``timing``
+        (True or a stride S): returns (ms of the bracketed launches, count)."""
         if self.colored is not None:
             raise RuntimeError("engine holds colour-major ratings; exact order "
                                "needs the original order")
@@ -227,35 +268,40 @@ class SGDEngine:
 
     def epoch_colored(self, seq: Optional[np.ndarray], lr: float, reg: float,
                       update_user: bool = True, update_item: bool = True,
-                      flags: int = _lib.MF_FLAG_XCD_SWIZZLE,
-                      timing: bool = False) -> Optional[float]:
-        """One epoch applying the colours in order ``seq`` (a permutation)."""
+                      flags: Optional[int] = None, timing=False):
+        """Apply the colours listed in ``seq`` in that order (a permutation of
+        all colours is one epoch; a prefix is a partial epoch)."""
         if self.colored is None:
             raise RuntimeError("call prepare_colored() first")
         if seq is not None:
             seq = np.ascontiguousarray(seq, np.int32)
+        if flags is None:
+            flags = default_sgd_flags()
         return self._run(None, self.colored, seq, lr, reg, update_user,
                          update_item, flags, timing)
 
     def _run(self, idx, offs, seq, lr, reg, update_user, update_item, flags, timing):
         nb = len(offs) - 1
-        ms = ctypes.c_double(0.0) if timing else None
+        nseq = 0 if seq is None else len(seq)
+        ms = (ctypes.c_double * 2)() if timing else None
+        if timing and timing is not True:
+            flags = int(flags) | (int(timing) << 16)       # timing = stride
         with torch.cuda.device(self.dev):
             if self.bias_only:
                 _lib.call("mf_bias_sgd_epoch", _tp(self.u), _tp(self.i), _tp(self.r),
-                          self.n, _tp(idx), _np(offs), _np(seq), nb,
+                          self.n, _tp(idx), _np(offs), nb, _np(seq), nseq,
                           self.global_mean, _tp(self.bu), _tp(self.bi), self.dcode,
                           float(lr), float(reg), int(update_user), int(update_item),
                           self.stream)
                 return None
             _lib.call("mf_sgd_epoch", _tp(self.u), _tp(self.i), _tp(self.r), self.n,
-                      _tp(idx), _np(offs), _np(seq), nb, self.global_mean,
+                      _tp(idx), _np(offs), nb, _np(seq), nseq, self.global_mean,
                       _tp(self.bu), _tp(self.bi), _tp(self.P), _tp(self.Q),
                       self.n_users, self.n_items, self.k, self.kcode, self.dcode,
                       self.gamma, float(lr), float(reg), self.min_rating,
                       self.max_rating, int(update_user), int(update_item), int(flags),
-                      self.stream, ctypes.byref(ms) if timing else None)
-        return ms.value if timing else None
+                      self.stream, ms)
+        return (ms[0], int(ms[1])) if timing else None
 
     # ---------------------------------------------------------- read-only
     def sse_async(self, slot: int) -> None:
@@ -268,10 +314,12 @@ class SGDEngine:
                           self.global_mean, _tp(self.bu), _tp(self.bi), self.dcode,
                           _tp(self.ws), out, self.stream)
             else:
-                _lib.call("mf_sse", _tp(self.u), _tp(self.i), _tp(self.r), self.n,
+                offs = self.eval_offs
+                _lib.call("mf_sse", _tp(self.eu), _tp(self.ei), _tp(self.er), self.n,
                           self.global_mean, _tp(self.bu), _tp(self.bi), _tp(self.P),
                           _tp(self.Q), self.k, self.kcode, self.dcode, self.gamma,
-                          self.min_rating, self.max_rating, _tp(self.ws), out,
+                          self.min_rating, self.max_rating, _np(offs),
+                          0 if offs is None else len(offs) - 1, _tp(self.ws), out,
                           self.stream)
 
     def sse_values(self, n_slots: int) -> np.ndarray:

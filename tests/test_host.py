@@ -49,7 +49,7 @@ def test_library_errors_are_reported():
     offs = np.array([0, 5], np.int64)
     # n_factors out of range -> MF_ERR_INVALID before any device work
     rc = lib.mf_sgd_epoch(None, None, None, 0, None, offs.ctypes.data_as(ctypes.c_void_p),
-                          None, 1, 0.0, None, None, None, None, 0, 0, 4096, 0, 0, 0.0,
+                          1, None, 0, 0.0, None, None, None, None, 0, 0, 4096, 0, 0, 0.0,
                           0.01, 0.02, 0.0, 5.0, 1, 1, 0, None, None)
     assert rc == 1 and "batch_offsets" in _lib.last_error() or "n_factors" in _lib.last_error()
     with pytest.raises(_lib.MFLibraryError):
