@@ -14,8 +14,8 @@ timed steps (inputs resident in HBM, max over ranks).
 
 Also reported (rank 0):
   roofline      SGD-kernel algorithmic bytes (16k+28 B per update, SURVEY
-                8d) / summed kernel time (hipEvents around every launch of
-                the timed steps) against 8 TB/s; `traffic` = measured HBM
+                8d) / SGD-phase time (one hipEvent pair around each timed
+                epoch's launches) against 8 TB/s; `traffic` = measured HBM
                 bytes per launch from rocprofv3 PMC (profiles/) or null;
   cpu_baseline  the CPU oracle (FP64 C port of the reference loop, 1 core)
                 on a bounded sample: the first colours of epoch 1 (~10M
@@ -102,9 +102,8 @@ def main() -> int:
     ap.add_argument("--reg", type=float, default=0.02)
     ap.add_argument("--cpu-sample", type=int, default=10_000_000,
                     help="ratings in the CPU-oracle sample (0 = skip the CPU leg)")
-    ap.add_argument("--timing-stride", type=int, default=8,
-                    help="bracket every N-th SGD launch of the timed epochs with "
-                         "hipEvents (0 = no kernel timing)")
+    ap.add_argument("--no-phase-timing", action="store_true",
+                    help="do not bracket the SGD / RMSE phases with hipEvents")
     args = ap.parse_args()
 
     import torch
@@ -218,22 +217,29 @@ def main() -> int:
 
     # ---------------- warmup + timed epochs
     reset_params()
-    stride = args.timing_stride
-    sizes = np.diff(eng.colored)
-    timed_ratings = []
+    phase = not args.no_phase_timing
+    launches_per_epoch = int(np.sum(np.diff(eng.colored) > 0))
+    events = []     # (sgd start, sgd end, sse end) per timed epoch
 
     def epoch(ep, timed):
+        # hipEvents on the stream the kernels run on (torch's current stream,
+        # which the engine launches on): one pair around the epoch's SGD
+        # launches, one more after the RMSE pass -- no host sync in the loop.
         seq = seq_for(ep)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if (timed and phase) else None
         if exch is not None:
             exch.begin_epoch()
-        ms = eng.epoch_colored(seq, args.lr, args.reg,
-                               timing=stride if (timed and stride > 0) else False)
+        if ev:
+            ev[0].record()
+        eng.epoch_colored(seq, args.lr, args.reg)
+        if ev:
+            ev[1].record()
         if exch is not None:
             exch.end_epoch()
         eng.sse_async(ep)
-        if ms is not None:
-            timed_ratings.append(int(sizes[seq[::stride]].sum()))
-        return ms
+        if ev:
+            ev[2].record()
+            events.append(ev)
 
     for ep in range(args.warmup):
         epoch(ep, False)
@@ -243,9 +249,8 @@ def main() -> int:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    kernel_ms = []
     for j in range(args.steps):
-        kernel_ms.append(epoch(args.warmup + j, True))
+        epoch(args.warmup + j, True)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -262,23 +267,27 @@ def main() -> int:
         value = nnz * args.steps / elapsed
         bytes_per_update = (16 * k + 28) if args.dtype == "float32" else (32 * k + 44)
         roofline = None
-        if stride > 0 and args.steps > 0:
-            ksum = float(sum(m[0] for m in kernel_ms)) / 1e3       # s, bracketed launches
-            launches = int(sum(m[1] for m in kernel_ms))
-            rated = int(sum(timed_ratings))
-            alg = bytes_per_update * rated                         # algorithmic bytes
-            achieved = alg / ksum / 1e9
+        phases = None
+        if events:
+            sgd_s = sum(e[0].elapsed_time(e[1]) for e in events) / 1e3
+            sse_s = sum(e[1].elapsed_time(e[2]) for e in events) / 1e3
+            launches = launches_per_epoch * len(events)
+            alg = bytes_per_update * n_local * len(events)         # algorithmic bytes
+            achieved = alg / sgd_s / 1e9
             traffic = traffic_from_profiles(args.workload, world)
             roofline = {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "k_sgd_batch",
-                "timed_launches": launches, "timing_stride": stride,
-                "avg_launch_us": ksum / launches * 1e6,
+                "kernel": "k_sgd_batch", "launches": launches,
+                "avg_launch_us": sgd_s / launches * 1e6,
+                "avg_launch_note": "SGD phase time / launches (includes ~1.3 us "
+                                   "inter-kernel gaps)",
                 "alg_bytes_per_launch": alg / launches,
                 "bytes_per_update": bytes_per_update,
-                "sgd_kernel_updates_per_s": rated / ksum,
             }
+            phases = {"sgd_ms_per_epoch": sgd_s / len(events) * 1e3,
+                      "rmse_ms_per_epoch": sse_s / len(events) * 1e3,
+                      "sgd_updates_per_s": n_local * len(events) / sgd_s}
         out = {
             "metric": METRIC, "value": value, "unit": "rating-updates/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -292,7 +301,8 @@ def main() -> int:
                        "parallelism": f"user-sharded dp{world}" if world > 1 else "single GPU",
                        "step": "one epoch: SGD sweep + training-RMSE pass"},
             "final_rmse": rmse[-1], "rmse_per_epoch": rmse,
-            "roofline": roofline, "cpu_baseline": cpu_baseline, "parity": parity,
+            "roofline": roofline, "phases": phases,
+            "cpu_baseline": cpu_baseline, "parity": parity,
             "schedule_build_s": t_sched,
         }
         print(json.dumps(out), flush=True)
