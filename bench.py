@@ -49,6 +49,9 @@ WORKLOADS = {
            "synthetic 100Kx10K 5M-nnz rank-32 sigmoid SGD"),
     "small": (100_000, 20_000, 4_000_000, 64, "linear",
               "synthetic 100Kx20K 4M-nnz rank-64 linear SGD (smoke)"),
+    # probes (not bench lines): P that fits the 256 MiB Infinity Cache
+    "c3_u250k": (250_000, 100_000, 100_000_000, 64, "linear",
+                 "probe: synthetic 250Kx100K 100M-nnz rank-64 linear SGD"),
 }
 
 

@@ -53,7 +53,9 @@ enum { MF_LINEAR = 0, MF_SIGMOID = 1, MF_RBF = 2 };
 enum {
     MF_FLAG_XCD_SWIZZLE = 1,  /* map consecutive tiles of a batch onto one XCD */
     MF_FLAG_NT_USER = 2,      /* stream user rows/biases/triples non-temporally */
-    MF_FLAG_NT_ITEM = 4       /* store item rows/biases non-temporally          */
+    MF_FLAG_NT_ITEM = 4,      /* (unused by the current kernels)                */
+    MF_FLAG_XCD_CLAIM = 8     /* workgroups claim the tiles of the item slice of
+                                 the XCD they run on (needs `workspace`)        */
 };
 
 const char* mf_last_error(void);
@@ -93,6 +95,9 @@ int mf_max_factors(void);
  *                  kernel_matrix_factorization.py:405-406)
  *   update_user_params / update_item_params   as _sgd (:336-337)
  *   flags          MF_FLAG_* bits; bits 16..23 = timing stride S (0 = 1)
+ *   workspace      device, nullable: >= mf_sgd_workspace_bytes(launches)
+ *                  bytes, required by MF_FLAG_XCD_CLAIM (tile counters,
+ *                  zeroed by the call on `stream`)
  *   kernel_ms      host, nullable, 2 doubles: when given, every S-th launch
  *                  is bracketed by hipEvents on `stream`, the stream is
  *                  synchronised, kernel_ms[0] = summed time (ms) of the
@@ -108,7 +113,9 @@ int mf_sgd_epoch(const int32_t* user_ids, const int32_t* item_ids,
                  int32_t kernel, int32_t dtype, double gamma, double lr,
                  double reg, double min_rating, double max_rating,
                  int32_t update_user_params, int32_t update_item_params,
-                 int32_t flags, void* stream, double* kernel_ms);
+                 int32_t flags, void* workspace, size_t workspace_bytes,
+                 void* stream, double* kernel_ms);
+size_t mf_sgd_workspace_bytes(int32_t n_launch);
 
 /*
  * Sum of squared training errors, sum_j (r_j - pred_j)^2, accumulated in

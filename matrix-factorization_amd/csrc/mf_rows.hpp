@@ -52,6 +52,7 @@ struct SgdArgs {
     int32_t upd_user;
     int32_t upd_item;
     int32_t swizzle;
+    int32_t* claim;         // nullable: 8 per-slice tile counters of this launch
     Hyper<T> h;
 };
 
@@ -162,6 +163,40 @@ __device__ __forceinline__ T lane_partial(const typename VecOf<T, W>::type (&p)[
     return s;
 }
 
+// ----------------------------------------------------- tile placement
+// A batch is item-sorted, so tile t of T covers item slice ~ t*8/T.  Static:
+// blocks b and b+8 share an XCD (observed round-robin dealing), so the
+// bijective swizzle gives every XCD a contiguous tile range -- but the XCD
+// that receives block 0 changes from launch to launch.  Claiming: the block
+// reads the XCD it actually runs on and takes the next tile of that XCD's
+// slice from a per-launch counter (stealing from the other slices when its
+// own is exhausted), so each XCD keeps revisiting the same slice of Q across
+// launches.  Every tile is claimed exactly once whatever the placement:
+// T blocks make T successful claims.
+__device__ __forceinline__ unsigned xcc_id() {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return v & 7u;
+}
+
+__device__ __forceinline__ int64_t claim_tile(int32_t* ctr, int64_t nt) {
+    __shared__ int64_t s_tile;
+    if (threadIdx.x == 0) {
+        const unsigned xcc = xcc_id();
+        int64_t tile = -1;
+        for (unsigned k = 0; k < 8 && tile < 0; ++k) {
+            const unsigned x = (xcc + k) & 7u;
+            const int64_t lo = nt * x / 8, hi = nt * (x + 1) / 8;
+            if (hi <= lo) continue;
+            const int t = atomicAdd(ctr + x, 1);
+            if (t < hi - lo) tile = lo + t;
+        }
+        s_tile = tile;
+    }
+    __syncthreads();
+    return s_tile;
+}
+
 // ------------------------------------------------------------- SGD batch
 // Wave w applies ratings [w*RPW, (w+1)*RPW) of the batch (RPW = S*R):
 //   1. lane j loads triple j and gathers b_u / b_i of rating j;
@@ -178,7 +213,8 @@ __global__ __launch_bounds__(kBlock) void k_sgd_batch(SgdArgs<T> A) {
     const int lane = threadIdx.x & (kWave - 1);
     const int g = lane / GS;
     const int l = lane % GS;
-    const int64_t blk = A.swizzle ? xcd_swizzle(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+    const int64_t blk = A.claim ? claim_tile(A.claim, gridDim.x)
+                      : A.swizzle ? xcd_swizzle(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
     const int64_t w0 = (blk * kWavesPerBlock + threadIdx.x / kWave) * RPW;
     if (w0 >= A.n) return;
     const int nw = (int)min((int64_t)RPW, A.n - w0);
@@ -435,6 +471,7 @@ struct SgdParams {
     double mu; void* bu; void* bi; void* P; void* Q; int32_t k; int32_t kernel;
     double gamma, lr, reg, lo, hi; int32_t uu, ui, flags;
     hipStream_t stream; double* kernel_ms;
+    int32_t* claim;         // nullable: nl x 8 tile counters (zeroed here)
 };
 
 struct SseParams {
@@ -472,8 +509,11 @@ struct SgdRun {
         a.Bu = static_cast<T*>(p.bu); a.Bi = static_cast<T*>(p.bi);
         a.k = p.k; a.upd_user = p.uu; a.upd_item = p.ui;
         a.swizzle = (p.flags & MF_FLAG_XCD_SWIZZLE) ? 1 : 0;
+        a.claim = nullptr;
         a.h = make_hyper<T>(p.mu, p.lr, p.reg, p.gamma, p.lo, p.hi);
         const bool nt = (p.flags & MF_FLAG_NT_USER) != 0;
+        if (p.claim) MF_HIP_CHECK(hipMemsetAsync(p.claim, 0, sizeof(int32_t) * 8 * (size_t)p.nl,
+                                                 p.stream));
         // optional timing: hipEvents around every `stride`-th launch
         const int stride = std::max(1, (p.flags >> 16) & 0xff);
         std::vector<hipEvent_t> ev;
@@ -490,6 +530,7 @@ struct SgdRun {
             if (a.n <= 0) continue;
             const int64_t waves = (a.n + RPW - 1) / RPW;
             const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock));
+            if (p.claim) a.claim = p.claim + 8 * (int64_t)s;
             const bool tm = p.kernel_ms && (s % stride == 0);
             if (tm) {
                 hipError_t e = hipEventRecord(ev[2 * (s / stride)], p.stream);

@@ -173,6 +173,10 @@ using namespace mf;
 
 extern "C" int mf_max_factors(void) { return kMaxFactors; }
 
+extern "C" size_t mf_sgd_workspace_bytes(int32_t n_launch) {
+    return n_launch > 0 ? sizeof(int32_t) * 8 * (size_t)n_launch : 0;
+}
+
 extern "C" int mf_sgd_epoch(const int32_t* user_ids, const int32_t* item_ids,
                             const void* ratings, int64_t n_ratings,
                             const int32_t* order, const int64_t* batch_offsets,
@@ -185,6 +189,7 @@ extern "C" int mf_sgd_epoch(const int32_t* user_ids, const int32_t* item_ids,
                             double min_rating, double max_rating,
                             int32_t update_user_params,
                             int32_t update_item_params, int32_t flags,
+                            void* workspace, size_t workspace_bytes,
                             void* stream, double* kernel_ms) {
     if (n_ratings < 0 || n_batches < 0 || n_users < 0 || n_items < 0 ||
         (batch_seq && n_seq < 0)) {
@@ -217,11 +222,20 @@ extern "C" int mf_sgd_epoch(const int32_t* user_ids, const int32_t* item_ids,
     }
     if (kernel_ms) { kernel_ms[0] = 0.0; kernel_ms[1] = 0.0; }
     if (n_launch == 0 || n_ratings == 0) return MF_OK;
+    int32_t* claim = nullptr;
+    if (flags & MF_FLAG_XCD_CLAIM) {
+        if (!workspace || workspace_bytes < mf_sgd_workspace_bytes(n_launch)) {
+            set_error("MF_FLAG_XCD_CLAIM needs a workspace of mf_sgd_workspace_bytes(%d) bytes",
+                      n_launch);
+            return MF_ERR_INVALID;
+        }
+        claim = static_cast<int32_t*>(workspace);
+    }
     SgdParams P{user_ids, item_ids, ratings, order, batch_offsets, batch_seq, n_launch,
                 global_mean, user_biases, item_biases, user_features, item_features,
                 n_factors, kernel, gamma, lr, reg, min_rating, max_rating,
                 update_user_params ? 1 : 0, update_item_params ? 1 : 0, flags,
-                (hipStream_t)stream, kernel_ms};
+                (hipStream_t)stream, kernel_ms, claim};
     if (dtype == MF_F32) return sgd_launch_f32(P);
     if (dtype == MF_F64) return sgd_launch_f64(P);
     set_error("unknown dtype code %d", dtype);

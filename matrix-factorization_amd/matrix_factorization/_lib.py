@@ -19,6 +19,7 @@ MF_LINEAR, MF_SIGMOID, MF_RBF = 0, 1, 2
 MF_FLAG_XCD_SWIZZLE = 1
 MF_FLAG_NT_USER = 2
 MF_FLAG_NT_ITEM = 4
+MF_FLAG_XCD_CLAIM = 8
 MF_ERR_CAPACITY = 3
 MF_DELTA_TAKE, MF_DELTA_APPLY = 0, 1
 KERNEL_CODES = {"linear": MF_LINEAR, "sigmoid": MF_SIGMOID, "rbf": MF_RBF}
@@ -39,7 +40,9 @@ SIGNATURES = {
         _F64, _P, _P, _P, _P,                         # mu, bu, bi, P, Q
         _I32, _I32, _I32,                             # n_users, n_items, k
         _I32, _I32, _F64, _F64, _F64, _F64, _F64,     # kernel dtype gamma lr reg min max
-        _I32, _I32, _I32, _P, _PD]),                  # upd_u upd_i flags stream kernel_ms
+        _I32, _I32, _I32, _P, ctypes.c_size_t,        # upd_u upd_i flags ws ws_bytes
+        _P, _PD]),                                    # stream kernel_ms
+    "mf_sgd_workspace_bytes": (ctypes.c_size_t, [_I32]),
     "mf_sse_workspace_bytes": (ctypes.c_size_t, [_I64]),
     "mf_sse": (ctypes.c_int, [
         _P, _P, _P, _I64, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _F64, _F64,

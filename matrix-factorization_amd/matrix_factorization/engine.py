@@ -280,6 +280,13 @@ class SGDEngine:
         return self._run(None, self.colored, seq, lr, reg, update_user,
                          update_item, flags, timing)
 
+    def _claim_ws(self, n_launch):
+        """Per-launch tile counters for MF_FLAG_XCD_CLAIM (8 int32 each)."""
+        need = 8 * max(n_launch, 1)
+        if getattr(self, "_claim", None) is None or self._claim.numel() < need:
+            self._claim = torch.zeros(need, dtype=torch.int32, device=self.dev)
+        return self._claim
+
     def _run(self, idx, offs, seq, lr, reg, update_user, update_item, flags, timing):
         nb = len(offs) - 1
         nseq = 0 if seq is None else len(seq)
@@ -300,6 +307,7 @@ class SGDEngine:
                       self.n_users, self.n_items, self.k, self.kcode, self.dcode,
                       self.gamma, float(lr), float(reg), self.min_rating,
                       self.max_rating, int(update_user), int(update_item), int(flags),
+                      _tp(self._claim_ws(nseq or nb)), 8 * 4 * max(nseq or nb, 1),
                       self.stream, ms)
         return (ms[0], int(ms[1])) if timing else None
 

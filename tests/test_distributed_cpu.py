@@ -1,0 +1,194 @@
+"""User-sharded data parallelism, rehearsed on CPU with gloo (world_size 2).
+
+The per-epoch exchange of matrix_factorization.distributed (snapshot ->
+local colored epoch -> delta -> all_reduce(SUM) -> apply) runs in two real
+processes over gloo.  The device sweeps are replaced by the CPU oracle and the
+replica arithmetic by torch on CPU tensors (test doubles, this file only); the
+sharding, schedules, collective and bookkeeping are the product code.  The
+result must equal a single-process simulation of the same algorithm.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+
+NU, NI, NNZ, K = 300, 80, 6000, 8
+LR, REG, EPOCHS, SEED = 0.02, 0.05, 3, 99
+
+
+def _data():
+    rs = np.random.RandomState(0)
+    keys = rs.choice(NU * NI, NNZ, replace=False)
+    u = (keys // NI).astype(np.int32)
+    i = (keys % NI).astype(np.int32)
+    r = rs.randint(1, 6, NNZ).astype(np.float64)
+    P0 = rs.normal(0, 0.1, (NU, K))
+    Q0 = rs.normal(0, 0.1, (NI, K))
+    return u, i, r, P0, Q0
+
+
+class CpuEngine:
+    """Test double of SGDEngine for the colored schedule (oracle sweeps)."""
+
+    def __init__(self, u, i, r, n_users, n_items, k, mu):
+        self.u_host, self.i_host, self.r_host = u, i, r
+        self.n, self.n_users, self.n_items, self.k = len(u), n_users, n_items, k
+        self.global_mean = mu
+        self.colored = None
+        self.sse_buf = torch.zeros(16, dtype=torch.float64)
+        self.tdt, self.dev = torch.float64, torch.device("cpu")
+        self.P = self.Q = self.bu = self.bi = None
+
+    def load_params(self, P=None, Q=None, bu=None, bi=None):
+        t = lambda a: torch.as_tensor(np.array(a, np.float64))  # noqa: E731
+        if P is not None:
+            self.P = t(P).reshape(self.n_users, self.k)
+        if Q is not None:
+            self.Q = t(Q).reshape(self.n_items, self.k)
+        if bu is not None:
+            self.bu = t(bu)
+        if bi is not None:
+            self.bi = t(bi)
+
+    def prepare_colored(self):
+        from matrix_factorization.engine import sched_color
+
+        sched, offs = sched_color(self.u_host, self.i_host, self.n_users, self.n_items)
+        self.u_host, self.i_host, self.r_host = (self.u_host[sched], self.i_host[sched],
+                                                 self.r_host[sched])
+        self.colored = offs
+        return len(offs) - 1
+
+    def epoch_colored(self, seq, lr, reg, timing=False):
+        order = np.concatenate([np.arange(self.colored[b], self.colored[b + 1])
+                                for b in seq]).astype(np.int64)
+        Q = self.Q.numpy()
+        bi = self.bi.numpy()
+        oracle.sgd_pass(self.u_host, self.i_host, self.r_host, self.global_mean,
+                        self.bu.numpy(), bi, self.P.numpy(), Q, lr=lr, reg=reg, order=order)
+
+    def sse_async(self, slot):
+        self.sse_buf[slot] = oracle.sse(self.u_host, self.i_host, self.r_host,
+                                        self.global_mean, self.bu.numpy(), self.bi.numpy(),
+                                        self.P.numpy(), self.Q.numpy())
+
+
+def _exchange_cls():
+    from matrix_factorization.distributed import ReplicaExchange
+
+    class CpuExchange(ReplicaExchange):
+        def _delta(self, mode):                       # mf_replica_delta on CPU
+            from matrix_factorization import _lib
+            if mode == _lib.MF_DELTA_TAKE:
+                self.flat.sub_(self.snap)
+            else:
+                self.flat.add_(self.snap)
+
+    return CpuExchange
+
+
+def _run_rank(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from matrix_factorization.distributed import (global_rmse, local_shard, shard_users,
+                                                  sharded_epochs)
+
+    u, i, r, P0, Q0 = _data()
+    mu = float(r.mean())
+    bounds = shard_users(u, NU, world)
+    lu, li, lr_ = local_shard(u, i, r, bounds, rank)
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    eng = CpuEngine(lu, li, lr_, hi - lo, NI, K, mu)
+    eng.load_params(P=P0[lo:hi], bu=np.zeros(hi - lo))
+    ex = _exchange_cls()(eng)
+    ex.bind(Q0, np.zeros(NI))
+    sharded_epochs(eng, ex, EPOCHS, LR, REG, SEED)
+    rm = global_rmse(eng, EPOCHS, NNZ)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), Q=eng.Q.numpy(), bi=eng.bi.numpy(),
+             P=eng.P.numpy(), bu=eng.bu.numpy(), lo=lo, hi=hi, rmse=np.array(rm))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _simulate(world):
+    """Single-process restatement of the same algorithm."""
+    from matrix_factorization.distributed import local_shard, shard_users
+
+    u, i, r, P0, Q0 = _data()
+    mu = float(r.mean())
+    bounds = shard_users(u, NU, world)
+    engs = []
+    for rank in range(world):
+        lu, li, lr_ = local_shard(u, i, r, bounds, rank)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        e = CpuEngine(lu, li, lr_, hi - lo, NI, K, mu)
+        e.load_params(P=P0[lo:hi], bu=np.zeros(hi - lo), Q=Q0, bi=np.zeros(NI))
+        e.prepare_colored()
+        engs.append(e)
+    Q = Q0.copy()
+    bi = np.zeros(NI)
+    sse = np.zeros(EPOCHS)
+    for ep in range(EPOCHS):
+        dQ = np.zeros_like(Q)
+        dbi = np.zeros_like(bi)
+        for e in engs:
+            e.Q = torch.as_tensor(Q.copy())
+            e.bi = torch.as_tensor(bi.copy())
+            nb = len(e.colored) - 1
+            seq = np.random.RandomState((SEED * 1000003 + ep) & 0x7FFFFFFF).permutation(nb)
+            e.epoch_colored(seq, LR, REG)
+            dQ += e.Q.numpy() - Q
+            dbi += e.bi.numpy() - bi
+        Q = Q + dQ
+        bi = bi + dbi
+        for e in engs:
+            e.Q = torch.as_tensor(Q.copy())
+            e.bi = torch.as_tensor(bi.copy())
+            e.sse_async(ep)
+            sse[ep] += float(e.sse_buf[ep])
+    return Q, bi, np.sqrt(sse / NNZ), engs, bounds
+
+
+def test_shard_users_balances_ratings():
+    from matrix_factorization.distributed import local_shard, shard_users
+
+    u, i, r, _, _ = _data()
+    for world in (1, 2, 3, 8):
+        b = shard_users(u, NU, world)
+        assert b[0] == 0 and b[-1] == NU and np.all(np.diff(b) >= 0)
+        sizes = [len(local_shard(u, i, r, b, k)[0]) for k in range(world)]
+        assert sum(sizes) == NNZ
+        assert max(sizes) - min(sizes) <= np.bincount(u).max() + NNZ // (world * 10) + 1
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_exchange_matches_simulation(tmp_path):
+    world = 2
+    mp.start_processes(_run_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    res = [dict(np.load(tmp_path / f"rank{k}.npz")) for k in range(world)]
+    # every rank ends with the same item replica
+    assert np.array_equal(res[0]["Q"], res[1]["Q"])
+    assert np.array_equal(res[0]["bi"], res[1]["bi"])
+    Q, bi, rmse, engs, bounds = _simulate(world)
+    assert np.max(np.abs(res[0]["Q"] - Q)) < 1e-12
+    assert np.max(np.abs(res[0]["bi"] - bi)) < 1e-12
+    for k in range(world):
+        assert np.max(np.abs(res[k]["P"] - engs[k].P.numpy())) < 1e-12
+    assert np.max(np.abs(res[0]["rmse"] - rmse)) < 1e-12
+    assert rmse[-1] < rmse[0]

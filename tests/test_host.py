@@ -50,7 +50,7 @@ def test_library_errors_are_reported():
     # n_factors out of range -> MF_ERR_INVALID before any device work
     rc = lib.mf_sgd_epoch(None, None, None, 0, None, offs.ctypes.data_as(ctypes.c_void_p),
                           1, None, 0, 0.0, None, None, None, None, 0, 0, 4096, 0, 0, 0.0,
-                          0.01, 0.02, 0.0, 5.0, 1, 1, 0, None, None)
+                          0.01, 0.02, 0.0, 5.0, 1, 1, 0, None, 0, None, None)
     assert rc == 1 and "batch_offsets" in _lib.last_error() or "n_factors" in _lib.last_error()
     with pytest.raises(_lib.MFLibraryError):
         _lib.call("mf_predict", None, None, -1, 0.0, None, None, None, None, 8, 0, 0, 0.0,
@@ -346,3 +346,17 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(_lib, "LIB_PATH", str(tmp_path / "nope.so"))
     with pytest.raises(_lib.MFLibraryError, match="not found"):
         _lib.load()
+
+
+def test_slice_order_groups_items_then_users():
+    from matrix_factorization.engine import sched_slices
+
+    nu, ni = 200, 64
+    u, i, r = _random_ratings(5, nu, ni, 5000)
+    sched, offs = sched_slices(u, i, nu, ni, 8)
+    assert np.array_equal(np.sort(sched), np.arange(len(u)))
+    assert offs[0] == 0 and offs[-1] == len(u) and len(offs) == 9
+    for x in range(8):
+        seg = sched[offs[x]:offs[x + 1]]
+        assert np.all(i[seg] * 8 // ni == x)          # one item slice
+        assert np.all(np.diff(u[seg]) >= 0)           # user-sorted inside it

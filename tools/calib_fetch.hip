@@ -18,6 +18,22 @@ __global__ void k_gather(const float* __restrict__ T, const int* __restrict__ id
     v += __shfl_xor(v, 1);
     if (lane == 0 && v == 12345.f) out[0] = v;   // keep the load alive
 }
+// 16-B lanes: 16 lanes per 256-B row, 4 rows per wave instruction (the
+// float4 layout of k_sgd_batch / k_sse_stream at k = 64)
+__global__ void k_gather4(const float4* __restrict__ T, const int* __restrict__ idx, int n,
+                          float* out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int row = t / 16, l = t & 15;
+    if (row >= n) return;
+    float4 v = T[(size_t)idx[row] * 16 + l];
+    if (v.x + v.y + v.z + v.w == 12345.f) out[0] = v.x;
+}
+__global__ void k_scatter4(float4* __restrict__ T, const int* __restrict__ idx, int n) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int row = t / 16, l = t & 15;
+    if (row >= n) return;
+    T[(size_t)idx[row] * 16 + l] = make_float4(l, l, l, l);
+}
 __global__ void k_scatter(float* __restrict__ T, const int* __restrict__ idx, int n) {
     const int w = (blockIdx.x * blockDim.x + threadIdx.x) / 64, lane = threadIdx.x & 63;
     if (w >= n) return;
@@ -37,6 +53,8 @@ int main() {
     for (int rep = 0; rep < 3; ++rep) {
         hipLaunchKernelGGL(k_gather, dim3(n / 4), dim3(256), 0, 0, T, idx, n, out);
         hipLaunchKernelGGL(k_scatter, dim3(n / 4), dim3(256), 0, 0, T, idx, n);
+        hipLaunchKernelGGL(k_gather4, dim3(n / 16), dim3(256), 0, 0, (const float4*)T, idx, n, out);
+        hipLaunchKernelGGL(k_scatter4, dim3(n / 16), dim3(256), 0, 0, (float4*)T, idx, n);
     }
     hipDeviceSynchronize();
     printf("known bytes per dispatch: gather read %zu, scatter write %zu (+ %d B of indices)\n",

@@ -47,11 +47,15 @@ def main():
     ap.add_argument("--bench-write", required=True)
     ap.add_argument("--key", default="c3/n1")
     ap.add_argument("--out", default="profiles/traffic.json")
+    ap.add_argument("--shape", default="x4", choices=["x1", "x4"],
+                    help="calibration kernels matching the bench kernels' access "
+                         "width: x1 = 4 B/lane (k_gather/k_scatter), x4 = 16 B/lane")
     args = ap.parse_args()
 
     known = 256 * (1 << 20)                       # bytes per calibration dispatch
-    f_tot, f_n = pick(per_kernel(args.calib_fetch, "FETCH_SIZE"), "k_gather")
-    w_tot, w_n = pick(per_kernel(args.calib_write, "WRITE_SIZE"), "k_scatter")
+    g, sc = ("k_gather4", "k_scatter4") if args.shape == "x4" else ("k_gather(", "k_scatter(")
+    f_tot, f_n = pick(per_kernel(args.calib_fetch, "FETCH_SIZE"), g)
+    w_tot, w_n = pick(per_kernel(args.calib_write, "WRITE_SIZE"), sc)
     cf = known / (f_tot / f_n * 1024.0)
     cw = known / (w_tot / w_n * 1024.0)
     res = {}
@@ -70,7 +74,7 @@ def main():
         out = json.load(open(args.out))
     out[args.key] = {
         "hbm_bytes_per_sgd_launch": res["sgd"]["fetch_bytes"] + res["sgd"]["write_bytes"],
-        "calibration": {"fetch_factor": cf, "write_factor": cw,
+        "calibration": {"shape": args.shape, "fetch_factor": cf, "write_factor": cw,
                         "known_bytes_per_dispatch": known},
         "kernels": res,
     }

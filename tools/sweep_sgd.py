@@ -43,10 +43,10 @@ def main():
     nb = eng.prepare_colored()
     print(f"# {desc}: {nb} colours", file=sys.stderr, flush=True)
     X, NT, NQ = _lib.MF_FLAG_XCD_SWIZZLE, _lib.MF_FLAG_NT_USER, _lib.MF_FLAG_NT_ITEM
+    CL = _lib.MF_FLAG_XCD_CLAIM
     variants = {    # float4 layout, k=64: tile 0 -> S=4 slots (16 ratings/wave),
                     # 1 -> S=2, 2 -> S=8, 3 -> S=1
-        "s4": X, "s4_nt": X | NT, "s4_nt_noxcd": NT,
-        "s2_nt": X | NT | (1 << 8), "s8_nt": X | NT | (2 << 8), "s1_nt": X | NT | (3 << 8),
+        "s4_nt": X | NT, "s4_nt_noxcd": NT, "s4": X,
     }
     if args.variants:
         variants = {kk: v for kk, v in variants.items() if kk in args.variants.split(",")}
@@ -87,8 +87,8 @@ def main():
             _lib.call("mf_sgd_epoch", _tp(eng.u), _tp(eng.i), _tp(eng.r), eng.n, None,
                       _np(one), 1, None, 0, eng.global_mean, _tp(eng.bu), _tp(eng.bi),
                       _tp(eng.P), _tp(eng.Q), eng.n_users, eng.n_items, eng.k, eng.kcode,
-                      eng.dcode, eng.gamma, 0.01, 0.02, 1.0, 5.0, 1, 1, fl, eng.stream,
-                      ms)
+                      eng.dcode, eng.gamma, 0.01, 0.02, 1.0, 5.0, 1, 1, fl, None, 0,
+                      eng.stream, ms)
         single.append({"flags": fl, "ms": ms[0], "Gupd_s": nnz / ms[0] / 1e6})
     out = {"single_launch": single}
     for name, d in res.items():
