@@ -81,14 +81,15 @@ def synth(n_users: int, n_items: int, nnz: int, seed: int = 20261015):
     return u, i, r
 
 
-def traffic_from_profiles(workload: str, n_gpus: int):
+def traffic_from_profiles(workload: str, n_gpus: int, schedule: str = "colored"):
     """HBM bytes per SGD launch measured by rocprofv3 PMC passes, if a
     summary for this workload was committed under profiles/."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        e = d.get(f"{workload}/n{n_gpus}")
+        key = f"{workload}/n{n_gpus}" if schedule == "colored" else f"{workload}/{schedule}/n{n_gpus}"
+        e = d.get(key)
         return None if e is None else float(e["hbm_bytes_per_sgd_launch"])
     except (OSError, ValueError, KeyError):
         return None
@@ -107,6 +108,9 @@ def main() -> int:
                     help="ratings in the CPU-oracle sample (0 = skip the CPU leg)")
     ap.add_argument("--no-phase-timing", action="store_true",
                     help="do not bracket the SGD / RMSE phases with hipEvents")
+    ap.add_argument("--schedule", default="strata", choices=["strata", "colored"],
+                    help="strata: B x B blocks, item slabs in LDS (mf_strata.hpp); "
+                         "colored: one launch per edge colour (mf_rows.hpp)")
     args = ap.parse_args()
 
     import torch
@@ -150,9 +154,20 @@ def main() -> int:
     eng = SGDEngine(lu, li, lr_, n_users_local, ni, k, kernel, args.dtype, dev,
                     gamma=1.0 / k, min_rating=1.0, max_rating=5.0, global_mean=mu)
     t0 = time.time()
-    nb = eng.prepare_colored()
+    strata = args.schedule == "strata"
+    if strata:
+        plan = eng.prepare_strata()
+        nb = plan.B
+        # ratings per stratum (launch) and the positions of a prefix of strata
+        strat_sizes = np.diff(plan.boff[:: plan.B])
+        sched_desc = (f"strata (B={nb}: {nb} launches/epoch, item slabs in LDS, "
+                      f"{int(plan.n_colours.max())} colours max per block)")
+    else:
+        nb = eng.prepare_colored()
+        strat_sizes = np.diff(eng.colored)
+        sched_desc = f"colored ({nb} conflict-free batches/epoch on rank 0)"
     t_sched = time.time() - t0
-    log(f"rank {rank}: {n_local} local ratings, {nb} colours, scheduled in {t_sched:.1f}s")
+    log(f"rank {rank}: {n_local} local ratings, {sched_desc}, scheduled in {t_sched:.1f}s")
     exch = ReplicaExchange(eng) if world > 1 else None
 
     def reset_params():
@@ -167,6 +182,21 @@ def main() -> int:
     def seq_for(ep):
         return np.random.RandomState((seed * 1000003 + ep) & 0x7FFFFFFF).permutation(nb).astype(np.int32)
 
+    def rot_for(ep):          # colour-rotation seed of a strata epoch
+        return (seed * 7919 + ep * 104729) & 0x7FFFFFFF
+
+    def run(ep, seq):
+        if strata:
+            eng.epoch_strata(seq, rot_for(ep), args.lr, args.reg)
+        else:
+            eng.epoch_colored(seq, args.lr, args.reg)
+
+    def serial(ep, seq):
+        if strata:
+            return plan.serial_order(seq, rot_for(ep)).astype(np.int64)
+        return np.concatenate([np.arange(eng.colored[b], eng.colored[b + 1])
+                               for b in seq]).astype(np.int64)
+
     # ---------------- CPU baseline + parity on a bounded sample (rank 0, N=1)
     cpu_baseline = None
     parity = None
@@ -175,21 +205,21 @@ def main() -> int:
         import oracle  # test infrastructure: checker and reported baseline only
 
         seq0 = seq_for(0)
-        sizes = np.diff(eng.colored)[seq0]
+        sizes = strat_sizes[seq0]
         m = int(np.searchsorted(np.cumsum(sizes), min(args.cpu_sample, n_local))) + 1
         m = min(m, nb)
         reset_params()
-        eng.epoch_colored(seq0[:m], args.lr, args.reg)
+        run(0, seq0[:m])
         Pg, Qg, bug, big = eng.params_numpy()
-        order = np.concatenate([np.arange(eng.colored[b], eng.colored[b + 1])
-                                for b in seq0[:m]]).astype(np.int64)
+        order = serial(0, seq0[:m])
         S = len(order)
         us, is_, rsmp = eng.u_host[order], eng.i_host[order], eng.r_host[order].astype(np.float64)
         P = P0.astype(np.float64)
         Q = Q0.astype(np.float64)
         bu = np.zeros(nu)
         bi = np.zeros(ni)
-        log(f"cpu oracle: {S} ratings ({m} colours), FP64, 1 thread")
+        unit_name = "strata" if strata else "colours"
+        log(f"cpu oracle: {S} ratings ({m} {unit_name}), FP64, 1 thread")
         t0 = time.perf_counter()
         oracle.sgd_pass(us, is_, rsmp, mu, bu, bi, P, Q, kernel=kernel, gamma=1.0 / k,
                         lr=args.lr, reg=args.reg, min_rating=1.0, max_rating=5.0)
@@ -204,7 +234,7 @@ def main() -> int:
         cpu_baseline = {
             "value": S / (t_sgd + t_sse), "unit": "rating-updates/s", "cores": 1,
             "kind": "port",
-            "sample": (f"first {m} of {nb} colours of epoch 1 = {S} ratings of the same "
+            "sample": (f"first {m} of {nb} {unit_name} of epoch 1 = {S} ratings of the same "
                        f"workload: FP64 sequential SGD sweep ({t_sgd:.1f}s) + RMSE pass "
                        f"({t_sse:.1f}s), oracle/mf_oracle.c"),
             "sgd_only": S / t_sgd,
@@ -221,7 +251,7 @@ def main() -> int:
     # ---------------- warmup + timed epochs
     reset_params()
     phase = not args.no_phase_timing
-    launches_per_epoch = int(np.sum(np.diff(eng.colored) > 0))
+    launches_per_epoch = nb if strata else int(np.sum(np.diff(eng.colored) > 0))
     events = []     # (sgd start, sgd end, sse end) per timed epoch
 
     def epoch(ep, timed):
@@ -234,7 +264,7 @@ def main() -> int:
             exch.begin_epoch()
         if ev:
             ev[0].record()
-        eng.epoch_colored(seq, args.lr, args.reg)
+        run(ep, seq)
         if ev:
             ev[1].record()
         if exch is not None:
@@ -268,20 +298,29 @@ def main() -> int:
 
     if rank == 0:
         value = nnz * args.steps / elapsed
-        bytes_per_update = (16 * k + 28) if args.dtype == "float32" else (32 * k + 44)
+        ts = 4 if args.dtype == "float32" else 8
+        if strata:
+            # per epoch: user row read + write and the triple per update, plus
+            # per stratum the item slab + item biases in and out and the
+            # user-bias slice in and out (mf_strata.hpp)
+            alg_epoch = (n_local * (2 * k * ts + 8 + ts)
+                         + nb * 2 * (ni * (k + 1) * ts + n_users_local * ts))
+        else:
+            alg_epoch = n_local * ((16 * k + 28) if ts == 4 else (32 * k + 44))
+        bytes_per_update = alg_epoch / n_local
         roofline = None
         phases = None
         if events:
             sgd_s = sum(e[0].elapsed_time(e[1]) for e in events) / 1e3
             sse_s = sum(e[1].elapsed_time(e[2]) for e in events) / 1e3
             launches = launches_per_epoch * len(events)
-            alg = bytes_per_update * n_local * len(events)         # algorithmic bytes
+            alg = alg_epoch * len(events)                           # algorithmic bytes
             achieved = alg / sgd_s / 1e9
-            traffic = traffic_from_profiles(args.workload, world)
+            traffic = traffic_from_profiles(args.workload, world, args.schedule)
             roofline = {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "k_sgd_batch", "launches": launches,
+                "kernel": "k_sgd_strata" if strata else "k_sgd_batch", "launches": launches,
                 "avg_launch_us": sgd_s / launches * 1e6,
                 "avg_launch_note": "SGD phase time / launches (includes ~1.3 us "
                                    "inter-kernel gaps)",
@@ -300,7 +339,7 @@ def main() -> int:
             "data": "synthetic",
             "config": {"workload": desc, "n_users": nu, "n_items": ni, "nnz": nnz,
                        "n_factors": k, "kernel": kernel, "lr": args.lr, "reg": args.reg,
-                       "schedule": f"colored ({nb} conflict-free batches/epoch on rank 0)",
+                       "schedule": sched_desc,
                        "parallelism": f"user-sharded dp{world}" if world > 1 else "single GPU",
                        "step": "one epoch: SGD sweep + training-RMSE pass"},
             "final_rmse": rmse[-1], "rmse_per_epoch": rmse,

@@ -36,6 +36,39 @@ __device__ __forceinline__ void st(X* p, X v) {
     else *p = v;
 }
 
+// User-row access policy POL of k_sgd_batch: 0 plain, 1 non-temporal
+// global ops, >= 2 buffer ops with explicit gfx950 cache-policy bits
+// (aux: sc0 = 1, nt = 2, sc1 = 16) -- table kPolAux, for the L2-residency
+// experiments of tools/sweep_sgd.py.
+struct PolAux { int ld, st; };
+constexpr PolAux kPolAux[8] = {{0, 0}, {0, 0}, {0, 0}, {2, 16}, {16, 16}, {17, 17}, {19, 19}, {2, 2}};
+constexpr int kBufDword3 = 0x00020000;     // raw buffer, gfx9 family
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint64_t bytes) {
+    const uint32_t nr = bytes > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)bytes;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)nr, kBufDword3);
+}
+template <int AUX, typename X>
+__device__ __forceinline__ X buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    if constexpr (sizeof(X) == 16)
+        return __builtin_bit_cast(X, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, AUX));
+    else if constexpr (sizeof(X) == 8)
+        return __builtin_bit_cast(X, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, AUX));
+    else
+        return __builtin_bit_cast(X, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, AUX));
+}
+template <int AUX, typename X>
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t off, X v) {
+    using U4 = __attribute__((ext_vector_type(4))) unsigned;
+    using U2 = __attribute__((ext_vector_type(2))) unsigned;
+    if constexpr (sizeof(X) == 16)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(U4, v), r, (int)off, 0, AUX);
+    else if constexpr (sizeof(X) == 8)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(U2, v), r, (int)off, 0, AUX);
+    else
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), r, (int)off, 0, AUX);
+}
+
 template <typename T>
 struct SgdArgs {
     const int32_t* u;
@@ -53,6 +86,7 @@ struct SgdArgs {
     int32_t upd_item;
     int32_t swizzle;
     int32_t* claim;         // nullable: 8 per-slice tile counters of this launch
+    uint64_t p_bytes;       // bytes of P (buffer-policy range; < 4 GiB when POL >= 2)
     Hyper<T> h;
 };
 
@@ -121,17 +155,25 @@ struct SlotsFor {
 // Gather the rows of S rating slots: all loads issued before any use;
 // indices clamped so no load sits behind a branch; vector slots past the
 // row end are zeroed afterwards.
-template <typename T, int W, int GS, int V, int S, bool NT>
+template <typename T, int W, int GS, int V, int S, int POL>
 __device__ __forceinline__ void gather_rows(const T* base, const int (&id)[S], int k, int kv, int l,
-                                            typename VecOf<T, W>::type (&out)[S][V]) {
+                                            typename VecOf<T, W>::type (&out)[S][V],
+                                            uint64_t bytes = 0) {
     using VT = typename VecOf<T, W>::type;
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t rs;
+    if constexpr (POL >= 2) rs = buf_rsrc(base, bytes);
 #pragma unroll
     for (int x = 0; x < S; ++x) {
         const VT* row = reinterpret_cast<const VT*>(base + (int64_t)id[x] * k);
 #pragma unroll
         for (int v = 0; v < V; ++v) {
             const int vi = v * GS + l;
-            out[x][v] = ld<NT>(row + (vi < kv ? vi : kv - 1));
+            const int vc = vi < kv ? vi : kv - 1;
+            if constexpr (POL >= 2)
+                out[x][v] = buf_ld<kPolAux[POL].ld, VT>(
+                    rs, (uint32_t)(((uint32_t)id[x] * (uint32_t)k + (uint32_t)(vc * W)) * sizeof(T)));
+            else
+                out[x][v] = ld<POL == 1>(row + vc);
         }
     }
 #pragma unroll
@@ -161,6 +203,53 @@ __device__ __forceinline__ T lane_partial(const typename VecOf<T, W>::type (&p)[
         }
     }
     return s;
+}
+
+// Per-rating SGD arithmetic shared by k_sgd_batch and k_sgd_strata (same
+// expression order as the reference, FP contraction off).  `s` = group-reduced
+// dot product / squared distance; returns the error e and the kernel's
+// derivative factor d (1 for linear).
+template <typename T, int KERN>
+__device__ __forceinline__ void sgd_error(T s, T bu, T bi, T r, const Hyper<T>& h, T& e, T& d) {
+    d = (T)1;
+    if constexpr (KERN == MF_LINEAR) {
+        const T pred = ((h.mu + bi) + bu) + s;                   // kernels.py:148-153
+        e = pred - r;                                            // :156
+    } else if constexpr (KERN == MF_SIGMOID) {
+        const T lin = ((h.mu + bu) + bi) + s;                    // kernels.py:226-228
+        const T ex = dexp<T>(-lin);
+        const T sg = (T)1 / ((T)1 + ex);                         // :229
+        const T pred = h.a + h.c * sg;                           // :230
+        e = pred - r;                                            // :233
+        d = (sg * sg) * ex;                                      // :236 (no c factor)
+    } else {
+        const T E = dexp<T>((-h.gamma) * s);                     // kernels.py:302-303
+        const T pred = h.a + h.c * E;                            // :304
+        e = pred - r;                                            // :307
+        d = ((T)2 * E) * h.gamma;                                // :310 (no c factor)
+    }
+}
+
+// kernels.py:159-163 (linear) / :239-245 (sigmoid); rbf has no biases
+template <typename T, int KERN>
+__device__ __forceinline__ T sgd_bias(T b, T e, T d, const Hyper<T>& h) {
+    if constexpr (KERN == MF_LINEAR) return b - h.lr * (e + h.reg * b);
+    else return b - h.lr * (e * d + h.reg * b);
+}
+
+// kernels.py:166-178 / :248-260 / :313-325
+template <typename T, int KERN, typename VT>
+__device__ __forceinline__ void sgd_rows(VT pf, VT qf, T e, T d, const Hyper<T>& h, VT& np, VT& nq) {
+    if constexpr (KERN == MF_LINEAR) {
+        np = pf - h.lr * (e * qf + h.reg * pf);
+        nq = qf - h.lr * (e * pf + h.reg * qf);
+    } else if constexpr (KERN == MF_SIGMOID) {
+        np = pf - h.lr * (e * (qf * d) + h.reg * pf);
+        nq = qf - h.lr * (e * (pf * d) + h.reg * qf);
+    } else {
+        np = pf - h.lr * (e * (d * (qf - pf)) + h.reg * pf);
+        nq = qf - h.lr * (e * (d * (pf - qf)) + h.reg * qf);
+    }
 }
 
 // ----------------------------------------------------- tile placement
@@ -203,13 +292,14 @@ __device__ __forceinline__ int64_t claim_tile(int32_t* ctr, int64_t nt) {
 //   2. all rows of all slots are loaded;
 //   3. per slot: dot product (DPP), update, predicated stores.
 // No two ratings of a batch share a row, so no slot reads another's write.
-template <typename T, int W, int GS, int V, int KERN, int S, bool NT>
+template <typename T, int W, int GS, int V, int KERN, int S, int POL>
 __global__ __launch_bounds__(kBlock) void k_sgd_batch(SgdArgs<T> A) {
     using VT = typename VecOf<T, W>::type;
     constexpr int R = kWave / GS;
     constexpr int RPW = S * R;
     static_assert(RPW <= kWave, "one lane per rating for the triple loads");
 
+    constexpr bool NT = POL != 0;
     const int lane = threadIdx.x & (kWave - 1);
     const int g = lane / GS;
     const int l = lane % GS;
@@ -250,8 +340,8 @@ __global__ __launch_bounds__(kBlock) void k_sgd_batch(SgdArgs<T> A) {
     }
     VT p[S][V], q[S][V];
     if (kv > 0) {
-        gather_rows<T, W, GS, V, S, NT>(A.P, uu, k, kv, l, p);
-        gather_rows<T, W, GS, V, S, false>(A.Q, ii, k, kv, l, q);
+        gather_rows<T, W, GS, V, S, POL>(A.P, uu, k, kv, l, p, A.p_bytes);
+        gather_rows<T, W, GS, V, S, 0>(A.Q, ii, k, kv, l, q);
     } else {
 #pragma unroll
         for (int x = 0; x < S; ++x)
@@ -269,50 +359,31 @@ __global__ __launch_bounds__(kBlock) void k_sgd_batch(SgdArgs<T> A) {
 #pragma unroll
     for (int x = 0; x < S; ++x) {
         const T s = group_sum<GS>(lane_partial<T, W, V, KERN>(p[x], q[x]));
-        T e, d = (T)1;
-        if constexpr (KERN == MF_LINEAR) {
-            const T pred = ((h.mu + bi[x]) + bu[x]) + s;             // kernels.py:148-153
-            e = pred - rr[x];                                        // :156
-        } else if constexpr (KERN == MF_SIGMOID) {
-            const T lin = ((h.mu + bu[x]) + bi[x]) + s;              // kernels.py:226-228
-            const T ex = dexp<T>(-lin);
-            const T sg = (T)1 / ((T)1 + ex);                         // :229
-            const T pred = h.a + h.c * sg;                           // :230
-            e = pred - rr[x];                                        // :233
-            d = (sg * sg) * ex;                                      // :236 (no c factor)
-        } else {
-            const T E = dexp<T>((-h.gamma) * s);                     // kernels.py:302-303
-            const T pred = h.a + h.c * E;                            // :304
-            e = pred - rr[x];                                        // :307
-            d = ((T)2 * E) * h.gamma;                                // :310 (no c factor)
-        }
+        T e, d;
+        sgd_error<T, KERN>(s, bu[x], bi[x], rr[x], h, e, d);
         const bool lead = have[x] && l == 0;
-        if constexpr (KERN == MF_LINEAR) {                           // kernels.py:159-163
-            if (A.upd_user && lead) st<NT>(A.Bu + uu[x], bu[x] - h.lr * (e + h.reg * bu[x]));
-            if (A.upd_item && lead) A.Bi[ii[x]] = bi[x] - h.lr * (e + h.reg * bi[x]);
-        } else if constexpr (KERN == MF_SIGMOID) {                   // kernels.py:239-245
-            if (A.upd_user && lead) st<NT>(A.Bu + uu[x], bu[x] - h.lr * (e * d + h.reg * bu[x]));
-            if (A.upd_item && lead) A.Bi[ii[x]] = bi[x] - h.lr * (e * d + h.reg * bi[x]);
+        if constexpr (KERN != MF_RBF) {
+            if (A.upd_user && lead) st<NT>(A.Bu + uu[x], sgd_bias<T, KERN>(bu[x], e, d, h));
+            if (A.upd_item && lead) A.Bi[ii[x]] = sgd_bias<T, KERN>(bi[x], e, d, h);
         }
         VT* pw = reinterpret_cast<VT*>(A.P + (int64_t)uu[x] * k);
         VT* qw = reinterpret_cast<VT*>(A.Q + (int64_t)ii[x] * k);
+        [[maybe_unused]] __amdgpu_buffer_rsrc_t prs;
+        if constexpr (POL >= 2) prs = buf_rsrc(A.P, A.p_bytes);
 #pragma unroll
         for (int v = 0; v < V; ++v) {
             const int vi = v * GS + l;
             if (!(have[x] && vi < kv)) continue;
-            const VT pf = p[x][v], qf = q[x][v];
             VT np, nq;
-            if constexpr (KERN == MF_LINEAR) {                       // kernels.py:166-178
-                np = pf - h.lr * (e * qf + h.reg * pf);
-                nq = qf - h.lr * (e * pf + h.reg * qf);
-            } else if constexpr (KERN == MF_SIGMOID) {               // kernels.py:248-260
-                np = pf - h.lr * (e * (qf * d) + h.reg * pf);
-                nq = qf - h.lr * (e * (pf * d) + h.reg * qf);
-            } else {                                                 // kernels.py:313-325
-                np = pf - h.lr * (e * (d * (qf - pf)) + h.reg * pf);
-                nq = qf - h.lr * (e * (d * (pf - qf)) + h.reg * qf);
+            sgd_rows<T, KERN>(p[x][v], q[x][v], e, d, h, np, nq);
+            if constexpr (POL >= 2) {
+                if (A.upd_user)
+                    buf_st<kPolAux[POL].st>(
+                        prs, (uint32_t)(((uint32_t)uu[x] * (uint32_t)k + (uint32_t)(vi * W)) * sizeof(T)),
+                        np);
+            } else {
+                if (A.upd_user) st<NT>(pw + vi, np);
             }
-            if (A.upd_user) st<NT>(pw + vi, np);
             if (A.upd_item) qw[vi] = nq;
         }
     }
@@ -374,8 +445,8 @@ __global__ __launch_bounds__(kBlock) void k_sse_stream(ReadArgs<T> A, SliceTab S
                     rr[x] = take_f<GS>(tr, src);
                 }
                 if (kv > 0) {
-                    gather_rows<T, W, GS, V, S, false>(A.P, uu, k, kv, l, p);
-                    gather_rows<T, W, GS, V, S, false>(A.Q, ii, k, kv, l, q);
+                    gather_rows<T, W, GS, V, S, 0>(A.P, uu, k, kv, l, p);
+                    gather_rows<T, W, GS, V, S, 0>(A.Q, ii, k, kv, l, q);
                 } else {
 #pragma unroll
                     for (int x = 0; x < S; ++x)
@@ -472,6 +543,7 @@ struct SgdParams {
     double gamma, lr, reg, lo, hi; int32_t uu, ui, flags;
     hipStream_t stream; double* kernel_ms;
     int32_t* claim;         // nullable: nl x 8 tile counters (zeroed here)
+    int64_t n_users;
 };
 
 struct SseParams {
@@ -486,21 +558,40 @@ struct SgdRun {
     const SgdParams& p;
 
     // flags bits 8..11: experimental slot count for the rank-64 FP32 layout
+    // flags bits 8..11: experimental slot count, bits 12..15: experimental
+    // user-row policy (kPolAux), both for the rank-64 FP32 linear layout only
     template <int W, int GS, int V, int KERN>
     int run() {
         constexpr int SD = SlotsFor<kWave / GS, V, W>::S;
+        const bool nt = (p.flags & MF_FLAG_NT_USER) != 0;
         if constexpr (std::is_same<T, float>::value && W == 4 && GS == 16 && V == 1) {
             switch ((p.flags >> 8) & 0xf) {
-                case 1: return go<W, GS, V, KERN, 2>();
-                case 2: return go<W, GS, V, KERN, 8>();
-                case 3: return go<W, GS, V, KERN, 1>();
+                case 1: return nt ? go<W, GS, V, KERN, 2, 1>() : go<W, GS, V, KERN, 2, 0>();
+                case 2: return nt ? go<W, GS, V, KERN, 8, 1>() : go<W, GS, V, KERN, 8, 0>();
+                case 3: return nt ? go<W, GS, V, KERN, 1, 1>() : go<W, GS, V, KERN, 1, 0>();
                 default: break;
             }
+            if constexpr (KERN == MF_LINEAR) {
+                const int pol = (p.flags >> 12) & 0xf;
+                if (pol >= 2 && (uint64_t)p.n_users * (uint64_t)p.k * sizeof(T) > 0xFFFFFFFFull) {
+                    set_error("user-row policy %d needs P < 4 GiB", pol);
+                    return MF_ERR_INVALID;
+                }
+                switch (pol) {
+                    case 2: return go<W, GS, V, KERN, SD, 2>();
+                    case 3: return go<W, GS, V, KERN, SD, 3>();
+                    case 4: return go<W, GS, V, KERN, SD, 4>();
+                    case 5: return go<W, GS, V, KERN, SD, 5>();
+                    case 6: return go<W, GS, V, KERN, SD, 6>();
+                    case 7: return go<W, GS, V, KERN, SD, 7>();
+                    default: break;
+                }
+            }
         }
-        return go<W, GS, V, KERN, SD>();
+        return nt ? go<W, GS, V, KERN, SD, 1>() : go<W, GS, V, KERN, SD, 0>();
     }
 
-    template <int W, int GS, int V, int KERN, int S>
+    template <int W, int GS, int V, int KERN, int S, int POL>
     int go() {
         constexpr int RPW = S * (kWave / GS);
         SgdArgs<T> a;
@@ -510,8 +601,8 @@ struct SgdRun {
         a.k = p.k; a.upd_user = p.uu; a.upd_item = p.ui;
         a.swizzle = (p.flags & MF_FLAG_XCD_SWIZZLE) ? 1 : 0;
         a.claim = nullptr;
+        a.p_bytes = (uint64_t)p.n_users * (uint64_t)p.k * sizeof(T);
         a.h = make_hyper<T>(p.mu, p.lr, p.reg, p.gamma, p.lo, p.hi);
-        const bool nt = (p.flags & MF_FLAG_NT_USER) != 0;
         if (p.claim) MF_HIP_CHECK(hipMemsetAsync(p.claim, 0, sizeof(int32_t) * 8 * (size_t)p.nl,
                                                  p.stream));
         // optional timing: hipEvents around every `stride`-th launch
@@ -536,10 +627,8 @@ struct SgdRun {
                 hipError_t e = hipEventRecord(ev[2 * (s / stride)], p.stream);
                 if (e != hipSuccess) { rc = hip_fail(e, "hipEventRecord"); break; }
             }
-            if (nt) hipLaunchKernelGGL((k_sgd_batch<T, W, GS, V, KERN, S, true>), grid,
-                                       dim3(kBlock), 0, p.stream, a);
-            else hipLaunchKernelGGL((k_sgd_batch<T, W, GS, V, KERN, S, false>), grid,
-                                    dim3(kBlock), 0, p.stream, a);
+            hipLaunchKernelGGL((k_sgd_batch<T, W, GS, V, KERN, S, POL>), grid, dim3(kBlock), 0,
+                               p.stream, a);
             if (tm) {
                 hipError_t e = hipEventRecord(ev[2 * (s / stride) + 1], p.stream);
                 if (e != hipSuccess) { rc = hip_fail(e, "hipEventRecord"); break; }

@@ -1,6 +1,7 @@
 // mf_rows_f32.hip -- float instantiations of the SGD-batch and SSE kernels
 // (split per dtype so the two halves compile in parallel).
 #include "mf_rows.hpp"
+#include "mf_strata.hpp"
 
 namespace mf {
 
@@ -11,6 +12,11 @@ int sgd_launch_f32(const SgdParams& p) {
 
 int sse_launch_f32(const SseParams& p) {
     SseRun<float> r{p};
+    return dispatch_rows<float>(p.k, p.kernel, r);
+}
+
+int strata_launch_f32(const StrataParams& p) {
+    StrataRun<float> r{p};
     return dispatch_rows<float>(p.k, p.kernel, r);
 }
 

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "mf_rows.hpp"
+#include "mf_strata.hpp"
 #include "mf_dispatch.hpp"
 
 namespace mf {
@@ -235,9 +236,71 @@ extern "C" int mf_sgd_epoch(const int32_t* user_ids, const int32_t* item_ids,
                 global_mean, user_biases, item_biases, user_features, item_features,
                 n_factors, kernel, gamma, lr, reg, min_rating, max_rating,
                 update_user_params ? 1 : 0, update_item_params ? 1 : 0, flags,
-                (hipStream_t)stream, kernel_ms, claim};
+                (hipStream_t)stream, kernel_ms, claim, n_users};
     if (dtype == MF_F32) return sgd_launch_f32(P);
     if (dtype == MF_F64) return sgd_launch_f64(P);
+    set_error("unknown dtype code %d", dtype);
+    return MF_ERR_INVALID;
+}
+
+extern "C" size_t mf_strata_lds_bytes(int32_t max_block_items, int32_t max_block_users,
+                                      int32_t n_factors, int32_t dtype) {
+    if (max_block_items < 0 || max_block_users < 0 || n_factors < 0) return 0;
+    return dtype == MF_F32 ? strata_lds_bytes<float>(max_block_items, max_block_users, n_factors)
+                           : strata_lds_bytes<double>(max_block_items, max_block_users, n_factors);
+}
+
+extern "C" int32_t mf_strata_lds_limit(void) { return kLdsLimit; }
+
+extern "C" int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_ids,
+                                   const void* ratings, int64_t n_ratings, int32_t n_blocks,
+                                   const int32_t* user_bounds, const int32_t* item_bounds,
+                                   const int64_t* block_offsets, const int32_t* colour_start,
+                                   const int32_t* colour_offsets, int32_t max_block_items,
+                                   int32_t max_block_users, const int32_t* strata_seq,
+                                   int32_t n_seq, uint32_t seed, double global_mean,
+                                   void* user_biases, void* item_biases, void* user_features,
+                                   void* item_features, int32_t n_users, int32_t n_items,
+                                   int32_t n_factors, int32_t kernel, int32_t dtype,
+                                   double gamma, double lr, double reg, double min_rating,
+                                   double max_rating, int32_t update_user_params,
+                                   int32_t update_item_params, int32_t flags, void* stream,
+                                   double* kernel_ms) {
+    if (n_ratings < 0 || n_blocks < 0 || n_seq < 0 || n_users < 0 || n_items < 0 ||
+        max_block_items < 0 || max_block_users < 0) {
+        set_error("negative size");
+        return MF_ERR_INVALID;
+    }
+    if (kernel_ms) { kernel_ms[0] = 0.0; kernel_ms[1] = 0.0; }
+    if (n_seq == 0 || n_ratings == 0) return MF_OK;
+    if (n_blocks == 0 || !strata_seq || !user_bounds || !item_bounds || !block_offsets ||
+        !colour_start || !colour_offsets || !user_ids || !item_ids || !ratings) {
+        set_error("NULL plan or triple array");
+        return MF_ERR_INVALID;
+    }
+    if ((int64_t)n_blocks * n_blocks >= ((int64_t)1 << 31)) {
+        set_error("n_blocks=%d too large", n_blocks);
+        return MF_ERR_INVALID;
+    }
+    for (int32_t t = 0; t < n_seq; ++t) {
+        if (strata_seq[t] < 0 || strata_seq[t] >= n_blocks) {
+            set_error("strata_seq[%d] = %d out of range [0, %d)", t, strata_seq[t], n_blocks);
+            return MF_ERR_INVALID;
+        }
+    }
+    if (!user_features || !item_features || (kernel != MF_RBF && (!user_biases || !item_biases))) {
+        set_error("NULL parameter array");
+        return MF_ERR_INVALID;
+    }
+    (void)flags;
+    StrataParams P{user_ids, item_ids, ratings, user_bounds, item_bounds, block_offsets,
+                   colour_start, colour_offsets, n_blocks, max_block_items, max_block_users,
+                   strata_seq, n_seq, seed, global_mean, user_biases, item_biases,
+                   user_features, item_features, n_factors, kernel, gamma, lr, reg,
+                   min_rating, max_rating, update_user_params ? 1 : 0,
+                   update_item_params ? 1 : 0, flags, (hipStream_t)stream, kernel_ms};
+    if (dtype == MF_F32) return strata_launch_f32(P);
+    if (dtype == MF_F64) return strata_launch_f64(P);
     set_error("unknown dtype code %d", dtype);
     return MF_ERR_INVALID;
 }

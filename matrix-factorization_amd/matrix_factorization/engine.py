@@ -129,6 +129,120 @@ def sched_slices(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int,
 N_SLICES = 8          # one item slice per XCD (MI355X: 8 XCDs x 4 MiB L2)
 
 
+# ------------------------------------------------------------ strata plan
+def strata_mix(seed: int, blk: int) -> int:
+    """First colour of block ``blk`` (mod its colour count) in the epoch with
+    ``seed`` -- the host mirror of mf_strata.hpp:strata_mix."""
+    m = 0xFFFFFFFF
+    x = (int(seed) ^ ((int(blk) * 0x9E3779B9) & m)) & m
+    x ^= x >> 16
+    x = (x * 0x85EBCA6B) & m
+    x ^= x >> 13
+    x = (x * 0xC2B2AE35) & m
+    x ^= x >> 16
+    return x
+
+
+def balanced_bounds(ids: np.ndarray, m: int, n_blocks: int, by_count: bool = True) -> np.ndarray:
+    """``n_blocks`` contiguous id ranges over [0, m): equal rating counts
+    (``by_count``) or equal id counts."""
+    if not by_count or len(ids) == 0:
+        return (np.arange(n_blocks + 1, dtype=np.int64) * m // n_blocks).astype(np.int32)
+    cum = np.cumsum(np.bincount(ids, minlength=m).astype(np.int64))
+    targets = np.arange(1, n_blocks, dtype=np.int64) * cum[-1] // n_blocks
+    cuts = np.searchsorted(cum, targets, side="left") + 1
+    b = np.concatenate([[0], np.minimum(cuts, m), [m]]).astype(np.int64)
+    return np.maximum.accumulate(b).astype(np.int32)
+
+
+class StrataPlan:
+    """Host + device form of a mf_sched_strata plan."""
+
+    def __init__(self, B, ubnd, ibnd, boff, cstart, coff, dev):
+        self.B = int(B)
+        self.ubnd, self.ibnd, self.boff, self.cstart, self.coff = ubnd, ibnd, boff, cstart, coff
+        self.max_items = int(np.diff(ibnd).max()) if B else 0
+        self.max_users = int(np.diff(ubnd).max()) if B else 0
+        to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        self.d_ubnd, self.d_ibnd, self.d_boff = to(ubnd), to(ibnd), to(boff)
+        self.d_cstart, self.d_coff = to(cstart), to(coff)
+
+    @property
+    def n_colours(self) -> np.ndarray:
+        return np.diff(self.cstart) - 1
+
+    def serial_order(self, seq, seed) -> np.ndarray:
+        """Plan positions in the order one epoch (strata ``seq``, ``seed``)
+        applies them: a sequential order the GPU result equals."""
+        B = self.B
+        out = []
+        for s in seq:
+            for w in range(B):
+                blk = int(s) * B + w
+                c0 = int(self.cstart[blk])
+                nc = int(self.cstart[blk + 1]) - c0 - 1
+                if nc <= 0:
+                    continue
+                base = int(self.boff[blk])
+                rot = strata_mix(seed, blk) % nc
+                for cc in range(nc):
+                    c = (rot + cc) % nc
+                    out.append(np.arange(base + self.coff[c0 + c], base + self.coff[c0 + c + 1]))
+        return np.concatenate(out) if out else np.empty(0, np.int64)
+
+
+def sched_strata(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int, n_blocks: int,
+                 ubnd: np.ndarray, ibnd: np.ndarray, user_gap: int = 1):
+    """mf_sched_strata: (rating indices in plan order, block offsets, colour
+    starts, colour offsets)."""
+    n = len(u)
+    u = np.ascontiguousarray(u, np.int32)
+    i = np.ascontiguousarray(i, np.int32)
+    ubnd = np.ascontiguousarray(ubnd, np.int32)
+    ibnd = np.ascontiguousarray(ibnd, np.int32)
+    BB = n_blocks * n_blocks
+    sched = np.empty(max(n, 1), np.int32)
+    boff = np.empty(BB + 1, np.int64)
+    cstart = np.empty(BB + 1, np.int32)
+    cap = max(BB * 24 + 1, 1024)
+    for _ in range(2):
+        coff = np.empty(cap, np.int32)
+        used = ctypes.c_int64(0)
+        rc = _lib.load().mf_sched_strata(_np(u), _np(i), n, n_users, n_items, n_blocks,
+                                         _np(ubnd), _np(ibnd), user_gap, _np(sched),
+                                         _np(boff), _np(cstart), _np(coff), cap,
+                                         ctypes.byref(used))
+        if rc == 0:
+            return sched[:n], boff, cstart, coff[: used.value].copy()
+        if used.value > cap:
+            cap = int(used.value)
+            continue
+        _lib.check(rc, "mf_sched_strata")
+    _lib.check(1, "mf_sched_strata")
+
+
+def choose_strata_blocks(u, i, n_users, n_items, k, dcode, max_blocks=None):
+    """B and the user / item bounds: B ~ sqrt(n / 1024) capped at 256 (one
+    workgroup per CU), raised until the largest block's LDS image fits."""
+    lib = _lib.load()
+    n = len(u)
+    B = int(min(256, max(1, np.sqrt(n / 1024.0))))
+    if max_blocks is not None:
+        B = min(B, int(max_blocks))
+    limit = lib.mf_strata_lds_limit()
+    while True:
+        ub = balanced_bounds(u, n_users, B)
+        for by_count in (True, False):
+            ib = balanced_bounds(i, n_items, B, by_count)
+            need = lib.mf_strata_lds_bytes(int(np.diff(ib).max()), int(np.diff(ub).max()),
+                                           k, dcode)
+            if need <= limit:
+                return B, ub, ib
+        if B >= max(n_items, 1) and B >= max(n_users, 1):
+            raise ValueError("strata schedule: a single item row does not fit in LDS")
+        B = int(np.ceil(B * 1.25)) + 1
+
+
 def default_sgd_flags() -> int:
     env = os.environ.get("MF_SGD_FLAGS")
     if env is not None:
@@ -179,6 +293,7 @@ class SGDEngine:
         self._upload_triples(self.u_host, self.i_host, self.r_host)
         self._build_eval()
         self.colored = None          # (offsets,) once prepare_colored() ran
+        self.strata = None           # StrataPlan once prepare_strata() ran
         ws = max(_lib.load().mf_sse_workspace_bytes(self.n), 8)
         self.ws = torch.empty((ws + 7) // 8, dtype=torch.float64, device=self.dev)
         self.sse_buf = torch.zeros(16, dtype=torch.float64, device=self.dev)
@@ -253,13 +368,55 @@ class SGDEngine:
         self.colored = offs
         return len(offs) - 1
 
+    def prepare_strata(self, n_blocks: Optional[int] = None, user_gap: int = 1) -> "StrataPlan":
+        """Build the stratified plan once and store the ratings in plan order
+        (block-major, colour-major inside a block)."""
+        if self.colored is not None or self.strata is not None:
+            raise RuntimeError("ratings already permuted by another schedule")
+        if n_blocks is None:
+            B, ub, ib = choose_strata_blocks(self.u_host, self.i_host, self.n_users,
+                                             self.n_items, self.k, self.dcode)
+        else:
+            B = int(n_blocks)
+            ub = balanced_bounds(self.u_host, self.n_users, B)
+            ib = balanced_bounds(self.i_host, self.n_items, B)
+        sched, boff, cstart, coff = sched_strata(self.u_host, self.i_host, self.n_users,
+                                                 self.n_items, B, ub, ib, user_gap)
+        self.u_host = self.u_host[sched]
+        self.i_host = self.i_host[sched]
+        self.r_host = self.r_host[sched]
+        self._upload_triples(self.u_host, self.i_host, self.r_host)
+        self.strata = StrataPlan(B, ub, ib, boff, cstart, coff, self.dev)
+        return self.strata
+
+    def epoch_strata(self, seq: Optional[np.ndarray], seed: int, lr: float, reg: float,
+                     update_user: bool = True, update_item: bool = True, timing=False):
+        """Apply the strata listed in ``seq`` (a permutation of range(B) is
+        one epoch) with colour rotation ``seed``."""
+        pl = self.strata
+        if pl is None:
+            raise RuntimeError("call prepare_strata() first")
+        seq = (np.arange(pl.B, dtype=np.int32) if seq is None
+               else np.ascontiguousarray(seq, np.int32))
+        ms = (ctypes.c_double * 2)() if timing else None
+        with torch.cuda.device(self.dev):
+            _lib.call("mf_sgd_epoch_strata", _tp(self.u), _tp(self.i), _tp(self.r), self.n,
+                      pl.B, _tp(pl.d_ubnd), _tp(pl.d_ibnd), _tp(pl.d_boff), _tp(pl.d_cstart),
+                      _tp(pl.d_coff), pl.max_items, pl.max_users, _np(seq), len(seq),
+                      int(seed) & 0xFFFFFFFF, self.global_mean, _tp(self.bu), _tp(self.bi),
+                      _tp(self.P), _tp(self.Q), self.n_users, self.n_items, self.k,
+                      self.kcode, self.dcode, self.gamma, float(lr), float(reg),
+                      self.min_rating, self.max_rating, int(update_user), int(update_item),
+                      0, self.stream, ms)
+        return (ms[0], int(ms[1])) if timing else None
+
     def epoch_exact(self, order: np.ndarray, lr: float, reg: float,
                     update_user: bool = True, update_item: bool = True,
                     timing=False):
         """One epoch in the given visit order (rating indices).  ``timing``
         (True or a stride S): returns (ms of the bracketed launches, count)."""
-        if self.colored is not None:
-            raise RuntimeError("engine holds colour-major ratings; exact order "
+        if self.colored is not None or self.strata is not None:
+            raise RuntimeError("engine holds permuted ratings; exact order "
                                "needs the original order")
         sched, offs = sched_levels(self.u_host, self.i_host, order, self.n_users,
                                    self.n_items, update_user, update_item)
@@ -422,7 +579,9 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
 
     exact:   draws ``np.random.shuffle`` on the row order every epoch
              (the reference's RNG stream, :371);
-    colored: draws ``np.random.permutation(n_colours)`` every epoch.
+    colored: draws ``np.random.permutation(n_colours)`` every epoch;
+    strata:  draws ``np.random.permutation(B)`` (stratum order) and a 32-bit
+             colour-rotation seed every epoch.
     """
     if schedule == "exact":
         order = (np.arange(engine.n, dtype=np.int64) if rng_order is None
@@ -431,16 +590,24 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
         if engine.colored is None:
             engine.prepare_colored()
         nb = len(engine.colored) - 1
+    elif schedule == "strata":
+        if engine.strata is None:
+            engine.prepare_strata()
+        nb = engine.strata.B
     else:
-        raise ValueError(f"schedule must be 'exact' or 'colored', got {schedule!r}")
+        raise ValueError(f"schedule must be 'exact', 'colored' or 'strata', got {schedule!r}")
     train_rmse = []
     for epoch in range(n_epochs):
         if schedule == "exact":
             np.random.shuffle(order)
             engine.epoch_exact(order, lr, reg, update_user, update_item)
-        else:
+        elif schedule == "colored":
             seq = np.random.permutation(nb).astype(np.int32)
             engine.epoch_colored(seq, lr, reg, update_user, update_item)
+        else:
+            seq = np.random.permutation(nb).astype(np.int32)
+            seed = int(np.random.randint(0, 2**31 - 1))
+            engine.epoch_strata(seq, seed, lr, reg, update_user, update_item)
         engine.sse_async(epoch)
         if verbose == 1:
             rmse = engine.rmse_values(epoch + 1)[epoch]

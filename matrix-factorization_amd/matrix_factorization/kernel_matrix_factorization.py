@@ -10,7 +10,10 @@ Three keyword arguments are new and default to the reference's behaviour:
 ``schedule``  "exact" (default): the reference's visit order every epoch,
               reproduced bit-for-bit up to dot-product summation order;
               "colored": a conflict-free edge-colouring schedule, a different
-              valid sequential order per epoch, for throughput at scale.
+              valid sequential order per epoch;
+              "strata": the stratified sweep (users x items cut into B x B
+              blocks, item slabs resident in LDS; mf_strata.hpp), also a
+              valid sequential order per epoch -- the throughput setting.
 ``device``    HIP device ("cuda", "cuda:1", ...); None = current device.
 """
 
@@ -43,8 +46,8 @@ class KernelMF(RecommenderBase):
                  schedule: str = "exact", device=None):
         if kernel not in ("linear", "sigmoid", "rbf"):
             raise ValueError("Kernel must be one of linear, sigmoid, or rbf")
-        if schedule not in ("exact", "colored"):
-            raise ValueError("schedule must be 'exact' or 'colored'")
+        if schedule not in ("exact", "colored", "strata"):
+            raise ValueError("schedule must be 'exact', 'colored' or 'strata'")
         canonical_dtype(dtype)
         super().__init__(min_rating=min_rating, max_rating=max_rating, verbose=verbose)
         self.n_factors = n_factors

@@ -1,0 +1,147 @@
+"""GPU parity of the stratified sweep (schedule='strata', mf_strata.hpp).
+
+A strata epoch applies the ratings in one sequential order (strata in the
+given order, blocks of a stratum in any order, colours of a block from the
+seeded rotation); StrataPlan.serial_order lists it.  The GPU result must equal
+the oracle's sequential sweep over that order:
+  FP64 parameters: max |diff| <= 1e-11 * max(1, |value|), RMSE <= 1e-12
+  FP32 state vs FP64 oracle: RMSE <= 1e-5 (the north-star bar)
+Every block holds several ratings per user, spread over different colours, so
+the colour barrier's ordering of user-row stores and loads is exercised.
+"""
+
+import numpy as np
+import pandas as pd
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, tol):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    assert a.shape == b.shape
+    scale = max(1.0, float(np.max(np.abs(b)))) if b.size else 1.0
+    err = float(np.max(np.abs(a - b))) if a.size else 0.0
+    assert err <= tol * scale, f"max |diff| {err:.3e} > {tol:.0e} * {scale:.3g}"
+
+
+def _synthetic(seed, n_users, n_items, nnz):
+    rs = np.random.RandomState(seed)
+    keys = rs.choice(n_users * n_items, nnz, replace=False)
+    u = (keys // n_items).astype(np.int32)
+    i = (keys % n_items).astype(np.int32)
+    r = rs.randint(1, 6, nnz).astype(np.float64)
+    return u, i, r
+
+
+def _engine(u, i, r, nu, ni, k, kernel, dtype, P, Q, bu, bi):
+    from matrix_factorization.engine import SGDEngine
+
+    eng = SGDEngine(u, i, r, nu, ni, k, kernel, dtype, "cuda:0", gamma=1.0 / max(k, 1),
+                    min_rating=1.0, max_rating=5.0, global_mean=float(r.mean()))
+    eng.load_params(P, Q, bu, bi)
+    return eng
+
+
+# FP64 LDS image per block: items/B * (k+1) * 8 B + users/B * 8 B <= 160 KiB
+@pytest.mark.parametrize("kernel,k,B,gap", [("linear", 64, 4, 1), ("sigmoid", 32, 3, 2),
+                                            ("rbf", 16, 5, 1), ("linear", 100, 8, 1),
+                                            ("sigmoid", 7, 2, 1), ("linear", 8, 1, 1)])
+def test_strata_epochs_equal_serialized_oracle(kernel, k, B, gap):
+    import oracle
+
+    nu, ni, nnz = 3000, 800, 120000
+    u, i, r = _synthetic(11, nu, ni, nnz)
+    rs = np.random.RandomState(12)
+    P = rs.normal(0, 0.1, (nu, k)); Q = rs.normal(0, 0.1, (ni, k))
+    bu = np.zeros(nu); bi = np.zeros(ni)
+    eng = _engine(u, i, r, nu, ni, k, kernel, "float64", P, Q, bu, bi)
+    plan = eng.prepare_strata(n_blocks=B, user_gap=gap)
+    assert plan.B == B
+    mu = eng.global_mean
+    hyp = dict(kernel=kernel, gamma=eng.gamma, min_rating=1.0, max_rating=5.0)
+    P2, Q2, bu2, bi2 = P.copy(), Q.copy(), bu.copy(), bi.copy()
+    for ep in range(2):
+        seq = rs.permutation(B).astype(np.int32)
+        seed = int(rs.randint(0, 2**31 - 1))
+        eng.epoch_strata(seq, seed, lr=0.01, reg=0.02)
+        order = plan.serial_order(seq, seed)
+        assert np.array_equal(np.sort(order), np.arange(nnz))
+        oracle.sgd_pass(eng.u_host, eng.i_host, eng.r_host, mu, bu2, bi2, P2, Q2,
+                        lr=0.01, reg=0.02, order=order, **hyp)
+    eng.sse_async(0)
+    Pg, Qg, bug, big = eng.params_numpy()
+    _close(Pg, P2, 1e-11)
+    _close(Qg, Q2, 1e-11)
+    _close(bug, bu2, 1e-11)
+    _close(big, bi2, 1e-11)
+    ro = oracle.rmse(eng.u_host, eng.i_host, eng.r_host, mu, bu2, bi2, P2, Q2, **hyp)
+    assert abs(eng.rmse_values(1)[0] - ro) < 1e-12
+
+
+def test_strata_partial_epoch_and_frozen_items():
+    """A prefix of the strata is a partial epoch; update_item=False leaves the
+    item rows and biases bit-identical (update_users, :234)."""
+    import oracle
+
+    nu, ni, nnz, k = 2000, 600, 60000, 64
+    u, i, r = _synthetic(21, nu, ni, nnz)
+    rs = np.random.RandomState(22)
+    P = rs.normal(0, 0.1, (nu, k)); Q = rs.normal(0, 0.1, (ni, k))
+    bu = rs.normal(0, 0.1, nu); bi = rs.normal(0, 0.1, ni)
+    eng = _engine(u, i, r, nu, ni, k, "linear", "float64", P, Q, bu, bi)
+    plan = eng.prepare_strata(n_blocks=6)
+    seq = np.array([4, 1, 5], np.int32)
+    eng.epoch_strata(seq, 7, lr=0.02, reg=0.05, update_item=False)
+    Pg, Qg, bug, big = eng.params_numpy()
+    assert np.array_equal(Qg, Q) and np.array_equal(big, bi)
+    P2, Q2, bu2, bi2 = P.copy(), Q.copy(), bu.copy(), bi.copy()
+    oracle.sgd_pass(eng.u_host, eng.i_host, eng.r_host, eng.global_mean, bu2, bi2, P2, Q2,
+                    kernel="linear", lr=0.02, reg=0.05, order=plan.serial_order(seq, 7),
+                    update_item=False, min_rating=1.0, max_rating=5.0)
+    _close(Pg, P2, 1e-11)
+    _close(bug, bu2, 1e-11)
+
+
+def test_strata_float32_large_slab_rmse_within_1e5():
+    """FP32 at rank 64 with ~500-item slabs (≈130 KB of LDS per workgroup)."""
+    import oracle
+
+    nu, ni, nnz, k = 3000, 2000, 150000, 64
+    u, i, r = _synthetic(31, nu, ni, nnz)
+    rs = np.random.RandomState(32)
+    P = rs.normal(0, 0.1, (nu, k)); Q = rs.normal(0, 0.1, (ni, k))
+    eng = _engine(u, i, r, nu, ni, k, "linear", "float32", P, Q, np.zeros(nu), np.zeros(ni))
+    plan = eng.prepare_strata(n_blocks=4)
+    assert plan.max_items >= 450
+    P2, Q2 = P.copy(), Q.copy()
+    bu2, bi2 = np.zeros(nu), np.zeros(ni)
+    for ep in range(3):
+        seq = rs.permutation(4).astype(np.int32)
+        eng.epoch_strata(seq, ep + 100, lr=0.01, reg=0.02)
+        eng.sse_async(ep)
+        oracle.sgd_pass(eng.u_host, eng.i_host, eng.r_host, eng.global_mean, bu2, bi2, P2, Q2,
+                        lr=0.01, reg=0.02, order=plan.serial_order(seq, ep + 100),
+                        min_rating=1.0, max_rating=5.0)
+    ro = oracle.rmse(eng.u_host, eng.i_host, eng.r_host, eng.global_mean, bu2, bi2, P2, Q2,
+                     min_rating=1.0, max_rating=5.0)
+    assert abs(eng.rmse_values(3)[2] - ro) < 1e-5
+
+
+def test_kernelmf_strata_fit_converges():
+    import matrix_factorization as mf
+
+    u, i, r = _synthetic(41, 4000, 1000, 200000)
+    X = pd.DataFrame({"user_id": u, "item_id": i})
+    hp = dict(n_factors=32, n_epochs=6, lr=0.01, reg=0.02, min_rating=1, max_rating=5,
+              verbose=0)
+    np.random.seed(5)
+    ms = mf.KernelMF(dtype="float32", schedule="strata", **hp).fit(X, pd.Series(r))
+    np.random.seed(5)
+    me = mf.KernelMF(dtype="float32", schedule="exact", **hp).fit(X, pd.Series(r))
+    assert np.all(np.diff(ms.train_rmse) < 0)
+    # a different (valid) visit order: same trajectory to within SGD noise
+    assert abs(ms.train_rmse[-1] - me.train_rmse[-1]) < 2e-3
+    pred = ms.predict(X.iloc[:100])
+    assert len(pred) == 100 and np.all(np.isfinite(pred))

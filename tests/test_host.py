@@ -360,3 +360,65 @@ def test_slice_order_groups_items_then_users():
         seg = sched[offs[x]:offs[x + 1]]
         assert np.all(i[seg] * 8 // ni == x)          # one item slice
         assert np.all(np.diff(u[seg]) >= 0)           # user-sorted inside it
+
+
+# ------------------------------------------------------------ strata plan
+@pytest.mark.parametrize("B,gap", [(1, 1), (3, 2), (8, 1)])
+def test_strata_plan_is_valid(B, gap):
+    """mf_sched_strata: a permutation; block (s, w) holds user range (w+s)%B
+    x item range w; every colour is a matching; user colours >= gap apart;
+    colour counts reach the largest degree inside the block (B = 1)."""
+    from matrix_factorization import engine as E
+
+    rs = np.random.RandomState(0)
+    nu, ni, n = 1500, 300, 30000
+    keys = rs.choice(nu * ni, n, replace=False)
+    u = (keys // ni).astype(np.int32)
+    i = (keys % ni).astype(np.int32)
+    ub = E.balanced_bounds(u, nu, B)
+    ib = E.balanced_bounds(i, ni, B)
+    sched, boff, cst, coff = E.sched_strata(u, i, nu, ni, B, ub, ib, gap)
+    assert np.array_equal(np.sort(sched), np.arange(n))
+    us, is_ = u[sched], i[sched]
+    for s in range(B):
+        for w in range(B):
+            blk = s * B + w
+            lo, hi = boff[blk], boff[blk + 1]
+            ubk = (w + s) % B
+            assert np.all((us[lo:hi] >= ub[ubk]) & (us[lo:hi] < ub[ubk + 1]))
+            assert np.all((is_[lo:hi] >= ib[w]) & (is_[lo:hi] < ib[w + 1]))
+            c0, nc = cst[blk], cst[blk + 1] - cst[blk] - 1
+            offs = coff[c0:c0 + nc + 1]
+            assert offs[0] == 0 and offs[-1] == hi - lo and np.all(np.diff(offs) >= 0)
+            col = np.repeat(np.arange(nc), np.diff(offs))
+            for c in range(nc):
+                a, b = lo + offs[c], lo + offs[c + 1]
+                assert len(set(us[a:b])) == b - a and len(set(is_[a:b])) == b - a
+            order = np.lexsort((col, us[lo:hi]))
+            same = np.diff(us[lo:hi][order]) == 0
+            assert np.all(np.diff(col[order])[same] >= gap)
+    if B == 1:
+        dmax = max(np.bincount(u).max(), np.bincount(i).max())
+        assert cst[1] - 1 == dmax
+
+
+def test_strata_serial_order_and_rejections():
+    from matrix_factorization import _lib
+    from matrix_factorization import engine as E
+
+    u = np.array([0, 0, 1, 2, 2, 3], np.int32)
+    i = np.array([0, 1, 1, 0, 2, 2], np.int32)
+    ub = np.array([0, 2, 4], np.int32)
+    ib = np.array([0, 1, 3], np.int32)
+    sched, boff, cst, coff = E.sched_strata(u, i, 4, 3, 2, ub, ib)
+    plan = E.StrataPlan.__new__(E.StrataPlan)
+    plan.B, plan.boff, plan.cstart, plan.coff = 2, boff, cst, coff
+    order = plan.serial_order([1, 0], 12345)
+    assert np.array_equal(np.sort(order), np.arange(6))
+    # stratum 1 first: its positions come before stratum 0's
+    assert set(order[: boff[4] - boff[2]]) == set(range(boff[2], boff[4]))
+    with pytest.raises(_lib.MFLibraryError):
+        E.sched_strata(u, i, 4, 3, 2, np.array([0, 3, 2], np.int32), ib)
+    with pytest.raises(_lib.MFLibraryError):
+        E.sched_strata(u, i, 4, 3, 2, ub, ib, user_gap=3)
+    assert E.strata_mix(0, 0) == 0 and E.strata_mix(1, 2) != E.strata_mix(2, 1)

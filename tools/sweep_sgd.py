@@ -48,6 +48,9 @@ def main():
                     # 1 -> S=2, 2 -> S=8, 3 -> S=1
         "s4_nt": X | NT, "s4_nt_noxcd": NT, "s4": X,
     }
+    # user-row cache policies (mf_rows.hpp kPolAux; flags bits 12..15)
+    for pol in range(2, 8):
+        variants[f"p{pol}"] = X | (pol << 12)
     if args.variants:
         variants = {kk: v for kk, v in variants.items() if kk in args.variants.split(",")}
     res = {kk: {"kernel_ms": [], "wall_ms": [], "wall_nt_ms": []} for kk in variants}
