@@ -4,8 +4,10 @@
 Workload (BASELINE.json configs[2], the HBM-roofline headline): synthetic
 1M users x 100K items, 100M unique ratings (1..5 drawn from the ML-100K
 histogram), rank-64 linear-kernel SGD, lr=0.01, reg=0.02, init N(0, 0.1),
-FP32 parameters, colored (conflict-free) schedule.  With --gpus N the same
-100M ratings are user-sharded over N ranks (configs[3]; total work fixed).
+FP32 parameters, strata schedule (B x B user/item blocks, item slabs in LDS,
+user-owned rating slots; --schedule colored: one launch per edge colour).
+With --gpus N the same 100M ratings are user-sharded over N ranks
+(configs[3]; total work fixed).
 
 One step = one epoch exactly as the reference's `_sgd` runs it
 (kernel_matrix_factorization.py:369-443): the SGD sweep over every rating
@@ -13,13 +15,17 @@ plus the training-RMSE pass.  value = ratings * steps / wall time of the
 timed steps (inputs resident in HBM, max over ranks).
 
 Also reported (rank 0):
-  roofline      SGD-kernel algorithmic bytes (16k+28 B per update, SURVEY
-                8d) / SGD-phase time (one hipEvent pair around each timed
-                epoch's launches) against 8 TB/s; `traffic` = measured HBM
+  roofline      SGD-kernel algorithmic HBM bytes / SGD-phase time (one
+                hipEvent pair around each timed epoch's launches) against
+                8 TB/s.  Algorithmic bytes: SURVEY 8(d)'s 16k+28 B per update
+                for the colored kernel; for strata the part of it that must
+                cross HBM (user row + triple + user bias per update, the item
+                slab per stratum; item rows live in LDS), with the 16k+28 B
+                equivalent rate reported beside it.  `traffic` = measured HBM
                 bytes per launch from rocprofv3 PMC (profiles/) or null;
   cpu_baseline  the CPU oracle (FP64 C port of the reference loop, 1 core)
-                on a bounded sample: the first colours of epoch 1 (~10M
-                ratings by default), SGD + RMSE over the sample;
+                on a bounded sample: the first strata (colours) of epoch 1
+                (~10M ratings by default), SGD + RMSE over the sample;
   parity        GPU (FP32) vs oracle (FP64) after that same partial epoch
                 from the same initial state: RMSE over the sample.
 """
@@ -158,10 +164,11 @@ def main() -> int:
     if strata:
         plan = eng.prepare_strata()
         nb = plan.B
-        # ratings per stratum (launch) and the positions of a prefix of strata
-        strat_sizes = np.diff(plan.boff[:: plan.B])
+        strat_sizes = plan.stratum_sizes()           # ratings per stratum (launch)
+        fill = n_local / max(plan.n_positions, 1)
         sched_desc = (f"strata (B={nb}: {nb} launches/epoch, item slabs in LDS, "
-                      f"{int(plan.n_colours.max())} colours max per block)")
+                      f"{plan.NS} user-owned slots x {int(plan.n_steps.max())} steps max "
+                      f"per block, {fill:.1%} slot fill)")
     else:
         nb = eng.prepare_colored()
         strat_sizes = np.diff(eng.colored)
@@ -299,14 +306,19 @@ def main() -> int:
     if rank == 0:
         value = nnz * args.steps / elapsed
         ts = 4 if args.dtype == "float32" else 8
+        # 16k+28 B per rating-update = triple + user and item
+        # rows read and written + both biases read and written.  The colored
+        # kernel moves all of it through HBM / the fabric; the strata kernel
+        # keeps item rows and biases in LDS, so its algorithmic HBM bytes are
+        # the user row read + write, the triple and the user bias per update,
+        # plus per stratum the item slab (+ item biases) in and out and the
+        # user-bias slice in and out (mf_strata.hpp) -- DESIGN.md section 4.
+        survey_per_update = (16 * k + 28) if ts == 4 else (32 * k + 44)
         if strata:
-            # per epoch: user row read + write and the triple per update, plus
-            # per stratum the item slab + item biases in and out and the
-            # user-bias slice in and out (mf_strata.hpp)
             alg_epoch = (n_local * (2 * k * ts + 8 + ts)
                          + nb * 2 * (ni * (k + 1) * ts + n_users_local * ts))
         else:
-            alg_epoch = n_local * ((16 * k + 28) if ts == 4 else (32 * k + 44))
+            alg_epoch = n_local * survey_per_update
         bytes_per_update = alg_epoch / n_local
         roofline = None
         phases = None
@@ -326,6 +338,11 @@ def main() -> int:
                                    "inter-kernel gaps)",
                 "alg_bytes_per_launch": alg / launches,
                 "bytes_per_update": bytes_per_update,
+                "survey_bytes_per_update": survey_per_update,
+                "survey_equivalent_gbs": survey_per_update * n_local * len(events) / sgd_s / 1e9,
+                "note": "achieved = HBM bytes the schedule must move (item rows live in "
+                        "LDS for strata); survey_equivalent_gbs = the 16k+28 B/update "
+                        "count of SURVEY 8(d) over the same time",
             }
             phases = {"sgd_ms_per_epoch": sgd_s / len(events) * 1e3,
                       "rmse_ms_per_epoch": sse_s / len(events) * 1e3,

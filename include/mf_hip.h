@@ -121,34 +121,40 @@ size_t mf_sgd_workspace_bytes(int32_t n_launch);
  * One epoch (or the strata listed in strata_seq) of the STRATIFIED sweep:
  * the throughput form of `_sgd`'s loop (kernel_matrix_factorization.py:
  * 371-425), same per-rating updates (kernels.py:108-327).  The plan comes
- * from mf_sched_strata: ratings (user_ids/item_ids/ratings, DEVICE) stored
- * in plan order, B user ranges and B item ranges (user_bounds/item_bounds,
- * DEVICE, B+1 each), block_offsets (DEVICE, B*B+1, block (s, w) = user range
- * (w+s) mod B x item range w at s*B + w), colour_start (DEVICE, B*B+1) and
- * colour_offsets (DEVICE).  Stratum strata_seq[t] (HOST, n_seq entries) is
- * one launch of B workgroups; workgroup w stages item range w (rows + biases)
- * and the bias slice of its user range in LDS and applies the block's colours
- * starting at colour (mix(seed, block) mod n_colours), one barrier apart.
+ * from mf_strata_plan_build: B user ranges and B item ranges
+ * (user_bounds/item_bounds, DEVICE, B+1 each); block (s, w) = user range
+ * (w+s) mod B x item range w is a grid of (block_steps[s*B+w+1] -
+ * block_steps[s*B+w]) steps x n_slots rating slots (block_steps: DEVICE,
+ * B*B+1); the triples (user_ids/item_ids/ratings, DEVICE, n_positions =
+ * block_steps[B*B] * n_slots each) are stored in plan order, an idle slot
+ * holding user id -1.  n_slots must equal mf_strata_slots(n_factors, dtype).
+ * Stratum strata_seq[t] (HOST, n_seq entries) is one launch of B
+ * workgroups; workgroup w stages item range w (rows + biases) and the bias
+ * slice of its user range in LDS and applies the block's steps starting at
+ * step (mix(seed, block) mod n_steps), one LDS barrier apart.
  * max_block_items / max_block_users size the LDS (mf_strata_lds_bytes must
  * not exceed mf_strata_lds_limit()).  kernel_ms (HOST, optional): elapsed ms
  * of the whole call and the launch count (synchronises).
  */
 int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_ids,
-                        const void* ratings, int64_t n_ratings, int32_t n_blocks,
+                        const void* ratings, int64_t n_positions, int32_t n_blocks,
                         const int32_t* user_bounds, const int32_t* item_bounds,
-                        const int64_t* block_offsets, const int32_t* colour_start,
-                        const int32_t* colour_offsets, int32_t max_block_items,
-                        int32_t max_block_users, const int32_t* strata_seq,
-                        int32_t n_seq, uint32_t seed, double global_mean,
-                        void* user_biases, void* item_biases, void* user_features,
-                        void* item_features, int32_t n_users, int32_t n_items,
-                        int32_t n_factors, int32_t kernel, int32_t dtype, double gamma,
-                        double lr, double reg, double min_rating, double max_rating,
-                        int32_t update_user_params, int32_t update_item_params,
-                        int32_t flags, void* stream, double* kernel_ms);
+                        const int64_t* block_steps, int32_t n_slots,
+                        int32_t max_block_items, int32_t max_block_users,
+                        const int32_t* strata_seq, int32_t n_seq, uint32_t seed,
+                        double global_mean, void* user_biases, void* item_biases,
+                        void* user_features, void* item_features, int32_t n_users,
+                        int32_t n_items, int32_t n_factors, int32_t kernel, int32_t dtype,
+                        double gamma, double lr, double reg, double min_rating,
+                        double max_rating, int32_t update_user_params,
+                        int32_t update_item_params, int32_t flags, void* stream,
+                        double* kernel_ms);
 size_t mf_strata_lds_bytes(int32_t max_block_items, int32_t max_block_users,
                            int32_t n_factors, int32_t dtype);
 int32_t mf_strata_lds_limit(void);
+/* Rating slots per step of the strata kernel for (n_factors, dtype); -1 on
+ * invalid arguments. */
+int32_t mf_strata_slots(int32_t n_factors, int32_t dtype);
 
 /*
  * Sum of squared training errors, sum_j (r_j - pred_j)^2, accumulated in
@@ -316,24 +322,31 @@ int mf_sched_slices(const int32_t* user_ids, const int32_t* item_ids,
                     int64_t* slice_offsets);
 
 /*
- * Plan of the stratified sweep (mf_sgd_epoch_strata).  user_bounds /
- * item_bounds (HOST, n_blocks+1 each, non-decreasing from 0 to n_users /
- * n_items) cut the ids into B contiguous ranges.  Outputs: sched_out[n] =
- * rating indices in plan order (block-major, colour-major inside a block,
- * block (s, w) at s*B + w), block_offsets[B*B+1], colour_start[B*B+1] and
- * colour_offsets[colour_cap] (per block: n_colours+1 offsets relative to the
- * block start; *n_colour_offsets = entries used; MF_ERR_INVALID if colour_cap
- * is too small, with the size needed in the message).  Inside a block the
- * colouring is greedy, item-major, each item starting at a rotating colour
- * (balanced colour sizes); a user's ratings in one block get colours at
- * least user_gap (1 or 2) apart.
+ * Plan of the stratified sweep (mf_sgd_epoch_strata), host only.
+ * user_bounds / item_bounds (HOST, n_blocks+1 each, non-decreasing from 0 to
+ * n_users / n_items) cut the ids into B contiguous ranges; block (s, w) =
+ * user range (w+s) mod B x item range w.  Inside a block every user is owned
+ * by one of n_slots rating slots (largest degree first onto the least loaded
+ * slot) and the ratings are edge-coloured as a bipartite (slot, item)
+ * multigraph with exactly D = max(slot load, item degree) colours, one step
+ * per colour: no step holds a slot or an item twice.
+ *   mf_strata_plan_build      plans all blocks into an opaque handle
+ *   mf_strata_plan_positions  n_positions = (total steps) * n_slots
+ *   mf_strata_plan_fetch      sched_out[n_positions] = rating index per
+ *                             position, -1 = idle slot (block-major, step-
+ *                             major, slot-minor); block_steps[B*B+1] = step
+ *                             offsets of the blocks
+ *   mf_strata_plan_free
  */
-int mf_sched_strata(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
-                    int32_t n_users, int32_t n_items, int32_t n_blocks,
-                    const int32_t* user_bounds, const int32_t* item_bounds,
-                    int32_t user_gap, int32_t* sched_out, int64_t* block_offsets,
-                    int32_t* colour_start, int32_t* colour_offsets,
-                    int64_t colour_cap, int64_t* n_colour_offsets);
+typedef struct mf_strata_plan mf_strata_plan;
+int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
+                         int32_t n_users, int32_t n_items, int32_t n_blocks,
+                         const int32_t* user_bounds, const int32_t* item_bounds,
+                         int32_t n_slots, mf_strata_plan** plan_out);
+int64_t mf_strata_plan_positions(const mf_strata_plan* plan);
+int mf_strata_plan_fetch(const mf_strata_plan* plan, int32_t* sched_out,
+                         int64_t* block_steps);
+void mf_strata_plan_free(mf_strata_plan* plan);
 
 #ifdef __cplusplus
 }

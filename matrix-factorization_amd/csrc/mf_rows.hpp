@@ -119,7 +119,7 @@ struct SliceTab {
 // kernels.py:21-105.  `s` = group-reduced dot product (linear/sigmoid) or
 // squared distance (rbf).
 template <typename T, int KERN>
-__device__ __forceinline__ T predict_one(T s, T bu, T bi, const Hyper<T>& h) {
+__device__ __forceinline__ T predict_one(T s, T bu, T bi, const Hyper<T> h) {
     if constexpr (KERN == MF_LINEAR) {
         return ((h.mu + bi) + bu) + s;                       // kernels.py:42-44
     } else if constexpr (KERN == MF_SIGMOID) {
@@ -210,7 +210,7 @@ __device__ __forceinline__ T lane_partial(const typename VecOf<T, W>::type (&p)[
 // dot product / squared distance; returns the error e and the kernel's
 // derivative factor d (1 for linear).
 template <typename T, int KERN>
-__device__ __forceinline__ void sgd_error(T s, T bu, T bi, T r, const Hyper<T>& h, T& e, T& d) {
+__device__ __forceinline__ void sgd_error(T s, T bu, T bi, T r, const Hyper<T> h, T& e, T& d) {
     d = (T)1;
     if constexpr (KERN == MF_LINEAR) {
         const T pred = ((h.mu + bi) + bu) + s;                   // kernels.py:148-153
@@ -232,14 +232,14 @@ __device__ __forceinline__ void sgd_error(T s, T bu, T bi, T r, const Hyper<T>& 
 
 // kernels.py:159-163 (linear) / :239-245 (sigmoid); rbf has no biases
 template <typename T, int KERN>
-__device__ __forceinline__ T sgd_bias(T b, T e, T d, const Hyper<T>& h) {
+__device__ __forceinline__ T sgd_bias(T b, T e, T d, const Hyper<T> h) {
     if constexpr (KERN == MF_LINEAR) return b - h.lr * (e + h.reg * b);
     else return b - h.lr * (e * d + h.reg * b);
 }
 
 // kernels.py:166-178 / :248-260 / :313-325
 template <typename T, int KERN, typename VT>
-__device__ __forceinline__ void sgd_rows(VT pf, VT qf, T e, T d, const Hyper<T>& h, VT& np, VT& nq) {
+__device__ __forceinline__ void sgd_rows(VT pf, VT qf, T e, T d, const Hyper<T> h, VT& np, VT& nq) {
     if constexpr (KERN == MF_LINEAR) {
         np = pf - h.lr * (e * qf + h.reg * pf);
         nq = qf - h.lr * (e * pf + h.reg * qf);

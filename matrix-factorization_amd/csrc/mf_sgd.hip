@@ -252,29 +252,41 @@ extern "C" size_t mf_strata_lds_bytes(int32_t max_block_items, int32_t max_block
 
 extern "C" int32_t mf_strata_lds_limit(void) { return kLdsLimit; }
 
+extern "C" int32_t mf_strata_slots(int32_t n_factors, int32_t dtype) {
+    if (n_factors < 0 || n_factors > kMaxFactors || (dtype != MF_F32 && dtype != MF_F64)) {
+        set_error("mf_strata_slots: n_factors=%d / dtype=%d invalid", n_factors, dtype);
+        return -1;
+    }
+    if (dtype == MF_F32) {
+        StrataSlots<float> f;
+        return dispatch_rows<float>(n_factors, MF_LINEAR, f);
+    }
+    StrataSlots<double> f;
+    return dispatch_rows<double>(n_factors, MF_LINEAR, f);
+}
+
 extern "C" int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_ids,
-                                   const void* ratings, int64_t n_ratings, int32_t n_blocks,
+                                   const void* ratings, int64_t n_positions, int32_t n_blocks,
                                    const int32_t* user_bounds, const int32_t* item_bounds,
-                                   const int64_t* block_offsets, const int32_t* colour_start,
-                                   const int32_t* colour_offsets, int32_t max_block_items,
-                                   int32_t max_block_users, const int32_t* strata_seq,
-                                   int32_t n_seq, uint32_t seed, double global_mean,
-                                   void* user_biases, void* item_biases, void* user_features,
-                                   void* item_features, int32_t n_users, int32_t n_items,
-                                   int32_t n_factors, int32_t kernel, int32_t dtype,
-                                   double gamma, double lr, double reg, double min_rating,
-                                   double max_rating, int32_t update_user_params,
-                                   int32_t update_item_params, int32_t flags, void* stream,
-                                   double* kernel_ms) {
-    if (n_ratings < 0 || n_blocks < 0 || n_seq < 0 || n_users < 0 || n_items < 0 ||
-        max_block_items < 0 || max_block_users < 0) {
+                                   const int64_t* block_steps, int32_t n_slots,
+                                   int32_t max_block_items, int32_t max_block_users,
+                                   const int32_t* strata_seq, int32_t n_seq, uint32_t seed,
+                                   double global_mean, void* user_biases, void* item_biases,
+                                   void* user_features, void* item_features, int32_t n_users,
+                                   int32_t n_items, int32_t n_factors, int32_t kernel,
+                                   int32_t dtype, double gamma, double lr, double reg,
+                                   double min_rating, double max_rating,
+                                   int32_t update_user_params, int32_t update_item_params,
+                                   int32_t flags, void* stream, double* kernel_ms) {
+    if (n_positions < 0 || n_blocks < 0 || n_seq < 0 || n_users < 0 || n_items < 0 ||
+        max_block_items < 0 || max_block_users < 0 || n_slots < 1) {
         set_error("negative size");
         return MF_ERR_INVALID;
     }
     if (kernel_ms) { kernel_ms[0] = 0.0; kernel_ms[1] = 0.0; }
-    if (n_seq == 0 || n_ratings == 0) return MF_OK;
-    if (n_blocks == 0 || !strata_seq || !user_bounds || !item_bounds || !block_offsets ||
-        !colour_start || !colour_offsets || !user_ids || !item_ids || !ratings) {
+    if (n_seq == 0 || n_positions == 0) return MF_OK;
+    if (n_blocks == 0 || !strata_seq || !user_bounds || !item_bounds || !block_steps ||
+        !user_ids || !item_ids || !ratings) {
         set_error("NULL plan or triple array");
         return MF_ERR_INVALID;
     }
@@ -293,8 +305,8 @@ extern "C" int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_
         return MF_ERR_INVALID;
     }
     (void)flags;
-    StrataParams P{user_ids, item_ids, ratings, user_bounds, item_bounds, block_offsets,
-                   colour_start, colour_offsets, n_blocks, max_block_items, max_block_users,
+    StrataParams P{user_ids, item_ids, ratings, user_bounds, item_bounds, block_steps,
+                   n_blocks, n_slots, max_block_items, max_block_users,
                    strata_seq, n_seq, seed, global_mean, user_biases, item_biases,
                    user_features, item_features, n_factors, kernel, gamma, lr, reg,
                    min_rating, max_rating, update_user_params ? 1 : 0,

@@ -5,14 +5,24 @@
 // s is the B blocks (ub = (w + s) mod B, ib = w), w = 0..B-1: they share no
 // user and no item, so one launch applies a whole stratum with workgroup w on
 // block w.  The workgroup stages its item slab Q[ib] (+ b_i) and the user-bias
-// slice b_u[ub] in LDS, sweeps the block's colours (conflict-free inside the
-// block, mf_sched_strata) with a workgroup barrier between colours -- user
-// rows P[u] gathered from / written to HBM, item rows read and written in LDS
-// -- and writes the slab back.  The epoch = the B strata in a caller-chosen
-// order; inside a block the colours run from a per-(seed, block) rotation.
-// Every such order is a sequential order of the ratings, so the result is
-// exactly the sequential sweep of that serialised order (kernels.py:108-327
-// per rating, kernel_matrix_factorization.py:371-425 per epoch).
+// slice b_u[ub] in LDS and walks the block's plan (mf_strata_sched.cpp): a
+// D x NS grid, one step per row, one rating SLOT per lane group.  Every user
+// of the block is owned by one slot, so a user row is only ever read and
+// written by the same lanes, in program order; a step holds each item at most
+// once, so the item rows in LDS need one LDS-only barrier per step.  The steps
+// run from a per-(seed, block) rotation.  Every such order is a sequential
+// order of the ratings, so the result is exactly the sequential sweep of that
+// serialised order (kernels.py:108-327 per rating,
+// kernel_matrix_factorization.py:371-425 per epoch).
+//
+// Software pipeline (per lane group, no global-memory barrier anywhere):
+//   step t   loads the triples of step t+2 and gathers the user rows of step
+//            t+1, then applies step t from registers (its rows arrived during
+//            step t-1) and the LDS slab.
+// A user row prefetched for step t+1 was read before step t's stores; when
+// the slot's user is the same in both steps the row just computed is
+// forwarded instead (the only read-after-write the prefetch can miss: older
+// stores precede the load in the same lanes' program order).
 //
 // Per update the HBM traffic is the user row read + write (2 * 4k B at FP32)
 // and the triple; the item slab (2 * n_items * 4k B per stratum) and the
@@ -27,9 +37,23 @@ constexpr int kStrataWaves = 16;                    // 1024-thread workgroups
 constexpr int kStrataThreads = kStrataWaves * kWave;
 constexpr int kLdsLimit = 160 * 1024;               // gfx950 LDS per CU
 
+// rating slots per lane group of one wave-instruction (16 waves x RPW slots):
+// two while a lane's share of a row is small (<= 32 B of floats, 16 B of
+// doubles), else one -- 1024-lane workgroups leave 128 registers per lane
+// for the two pipeline stages
+template <typename T, int W, int GS, int V>
+constexpr int strata_group_slots() {
+    constexpr int bytes = W * V * (int)sizeof(T);
+    return ((kWave / GS) < 8 && bytes <= (sizeof(T) == 4 ? 32 : 16)) ? 2 : 1;
+}
+template <typename T, int W, int GS, int V>
+constexpr int strata_slots() {
+    return kStrataWaves * strata_group_slots<T, W, GS, V>() * (kWave / GS);
+}
+
 template <typename T>
 struct StrataArgs {
-    const int32_t* u;
+    const int32_t* u;        // plan order, NS per step; u < 0 = idle slot
     const int32_t* i;
     const T* r;
     T* P;
@@ -38,9 +62,7 @@ struct StrataArgs {
     T* Bi;
     const int32_t* ubnd;     // B + 1 user-range bounds
     const int32_t* ibnd;     // B + 1 item-range bounds
-    const int64_t* boff;     // B*B + 1: block (s, w) at s*B + w
-    const int32_t* cstart;   // B*B + 1: first colour offset of each block
-    const int32_t* coff;     // colour offsets, relative to the block start
+    const int64_t* bstep;    // B*B + 1 step offsets: block (s, w) at s*B + w
     int32_t B;
     int32_t s;
     uint32_t seed;
@@ -50,7 +72,7 @@ struct StrataArgs {
     Hyper<T> h;
 };
 
-// first colour of block `blk` in this epoch (mirrored by engine.strata_rotation)
+// first step of block `blk` in this epoch (mirrored by engine.strata_mix)
 __host__ __device__ inline uint32_t strata_mix(uint32_t seed, uint32_t blk) {
     uint32_t x = seed ^ (blk * 0x9E3779B9u);
     x ^= x >> 16;
@@ -66,13 +88,21 @@ __host__ __device__ inline size_t strata_lds_bytes(int max_items, int max_users,
     return sizeof(T) * ((size_t)max_items * (size_t)k + (size_t)max_items + (size_t)max_users);
 }
 
+// Orders the LDS accesses of the workgroup only: global loads and stores in
+// flight are not waited for (the pipeline keeps them in flight across steps).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 template <typename T, int W, int GS, int V, int KERN, int S>
 __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata(StrataArgs<T> A) {
     using VT = typename VecOf<T, W>::type;
     constexpr int R = kWave / GS;
     constexpr int RPW = S * R;
-    constexpr int PASS = kStrataWaves * RPW;
-    static_assert(RPW <= kWave, "one lane per rating for the triple loads");
+    constexpr int NS = kStrataWaves * RPW;
+    static_assert(RPW <= kWave, "one lane per rating slot for the triple loads");
     extern __shared__ __align__(16) unsigned char smem[];
 
     const int B = A.B;
@@ -83,7 +113,11 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata(StrataArgs<T> A) 
     const int ulo = A.ubnd[ub], nus = A.ubnd[ub + 1] - ulo;
     const int k = A.k;
     const int kv = k / W;
-    const Hyper<T> h = A.h;
+    // field by field: an aggregate copy of the kernel-argument struct ends up
+    // in scratch once the step lambda captures it
+    Hyper<T> h;
+    h.mu = A.h.mu; h.lr = A.h.lr; h.reg = A.h.reg; h.gamma = A.h.gamma;
+    h.a = A.h.a; h.c = A.h.c; h.lo = A.h.lo; h.hi = A.h.hi;
     T* Qs = reinterpret_cast<T*>(smem);
     T* Bis = Qs + (size_t)nqi * k;
     T* Bus = Bis + nqi;
@@ -106,94 +140,123 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata(StrataArgs<T> A) 
     const int wv = threadIdx.x / kWave;
     const int g = lane / GS;
     const int l = lane % GS;
-    const int c0 = A.cstart[blk];
-    const int nc = A.cstart[blk + 1] - c0 - 1;
-    const int64_t base = A.boff[blk];
-    int c = nc > 0 ? (int)(strata_mix(A.seed, (uint32_t)blk) % (uint32_t)nc) : 0;
+    const int64_t st0 = A.bstep[blk];
+    const int nst = (int)(A.bstep[blk + 1] - st0);
+    const int rot = nst > 0 ? (int)(strata_mix(A.seed, (uint32_t)blk) % (uint32_t)nst) : 0;
+    // position of this lane's slot in step 0 of the block
+    const int64_t lpos = st0 * NS + wv * RPW + (lane < RPW ? lane : 0);
+    auto pos_of = [&](int t) __attribute__((always_inline)) -> int64_t {
+        int c = rot + t;
+        if (c >= nst) c -= nst;
+        return lpos + (int64_t)c * NS;
+    };
 
-    for (int cc = 0; cc < nc; ++cc) {
-        const int64_t ca = base + A.coff[c0 + c], cb = base + A.coff[c0 + c + 1];
-        for (int64_t p0 = ca + (int64_t)wv * RPW; p0 < cb; p0 += PASS) {
-            const int nw = (int)min((int64_t)RPW, cb - p0);
-            int tu, ti;
-            T tr, tbu = (T)0, tbi = (T)0;
-            {
-                const int64_t j = p0 + (lane < nw ? lane : 0);
-                tu = ld<true>(A.u + j);
-                ti = ld<true>(A.i + j);
-                tr = ld<true>(A.r + j);
-            }
-            int uu[S], ii[S];
-            bool have[S];
-            T rr[S];
+    // Pipeline state, two copies used alternately (the loop is unrolled by
+    // two so no register holding an in-flight load is ever copied):
+    //   Tri   the triple of this lane's slot for one step
+    //   Rows  the broadcast ids, rating and gathered user rows of one step
+    struct Tri { int u, i; T r; };
+    struct Rows { int u[S], i[S]; bool have[S]; T r[S]; VT p[S][V]; };
+    // Every load is issued unconditionally (past the last step: a re-read of
+    // the last step, never applied): a load behind a branch would make the
+    // compiler drain the whole memory counter where its result is used.
+    auto load_tri = [&](int t, Tri& o) __attribute__((always_inline)) {
+        const int64_t j = pos_of(t < nst ? t : nst - 1);
+        o.u = ld<true>(A.u + j); o.i = ld<true>(A.i + j); o.r = ld<true>(A.r + j);
+    };
+    // slot x of lane group g <- triple lane x*R + g; idle slots point at a
+    // valid row (first user of the range, slab row 0) and never store.  Row
+    // tails past k are masked where the rows are used, not here: a register
+    // write would wait for the load in flight.
+    auto unpack_gather = [&](const Tri& tr, Rows& o) __attribute__((always_inline)) {
 #pragma unroll
-            for (int x = 0; x < S; ++x) {
-                const int idx = x * R + g;
-                have[x] = idx < nw;
-                const int src = have[x] ? idx : 0;
-                uu[x] = take_i<GS>(tu, src);
-                ii[x] = take_i<GS>(ti, src) - ilo;           // slab row
-                rr[x] = take_f<GS>(tr, src);
-            }
-            VT p[S][V], q[S][V];
-            if (kv > 0) {
-                gather_rows<T, W, GS, V, S, 1>(A.P, uu, k, kv, l, p);
+        for (int x = 0; x < S; ++x) {
+            const int src = x * R + g;
+            const int uv = take_i<GS>(tr.u, src);
+            const int iv = take_i<GS>(tr.i, src);
+            o.have[x] = uv >= 0;
+            o.u[x] = o.have[x] ? uv : ulo;
+            o.i[x] = o.have[x] ? iv - ilo : 0;
+            o.r[x] = take_f<GS>(tr.r, src);
+        }
 #pragma unroll
-                for (int x = 0; x < S; ++x) {
-                    const VT* row = reinterpret_cast<const VT*>(Qs + (size_t)ii[x] * k);
+        for (int x = 0; x < S; ++x) {
+            const VT* row = reinterpret_cast<const VT*>(A.P + (int64_t)o.u[x] * k);
 #pragma unroll
-                    for (int v = 0; v < V; ++v) {
-                        const int vi = v * GS + l;
-                        q[x][v] = vi < kv ? row[vi] : (VT)(T)0;
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int x = 0; x < S; ++x)
-#pragma unroll
-                    for (int v = 0; v < V; ++v) p[x][v] = q[x][v] = (VT)(T)0;
-            }
-            if constexpr (KERN != MF_RBF) {
-                tbu = Bus[tu - ulo];
-                tbi = Bis[ti - ilo];
-            }
-            T bu[S], bi[S];
-#pragma unroll
-            for (int x = 0; x < S; ++x) {
-                const int src = have[x] ? x * R + g : 0;
-                bu[x] = KERN != MF_RBF ? take_f<GS>(tbu, src) : (T)0;
-                bi[x] = KERN != MF_RBF ? take_f<GS>(tbi, src) : (T)0;
-            }
-#pragma unroll
-            for (int x = 0; x < S; ++x) {
-                const T sm = group_sum<GS>(lane_partial<T, W, V, KERN>(p[x], q[x]));
-                T e, d;
-                sgd_error<T, KERN>(sm, bu[x], bi[x], rr[x], h, e, d);
-                const bool lead = have[x] && l == 0;
-                if constexpr (KERN != MF_RBF) {
-                    if (A.upd_user && lead) Bus[uu[x] - ulo] = sgd_bias<T, KERN>(bu[x], e, d, h);
-                    if (A.upd_item && lead) Bis[ii[x]] = sgd_bias<T, KERN>(bi[x], e, d, h);
-                }
-                VT* pw = reinterpret_cast<VT*>(A.P + (int64_t)uu[x] * k);
-                VT* qw = reinterpret_cast<VT*>(Qs + (size_t)ii[x] * k);
-#pragma unroll
-                for (int v = 0; v < V; ++v) {
-                    const int vi = v * GS + l;
-                    if (!(have[x] && vi < kv)) continue;
-                    VT np, nq;
-                    sgd_rows<T, KERN>(p[x][v], q[x][v], e, d, h, np, nq);
-                    if (A.upd_user) st<true>(pw + vi, np);
-                    if (A.upd_item) qw[vi] = nq;
-                }
+            for (int v = 0; v < V; ++v) {
+                const int vi = v * GS + l;
+                o.p[x][v] = ld<true>(row + (vi < kv ? vi : kv - 1));     // kv >= 1
             }
         }
-        if (++c == nc) c = 0;
-        // The next colour may touch a user row written in this one: the
-        // workgroup barrier orders the (same-CU) global stores before the
-        // next loads, and the LDS slab writes before the next LDS reads.
-        __syncthreads();
+    };
+    int uprev[S];
+    VT pprev[S][V];
+#pragma unroll
+    for (int x = 0; x < S; ++x) uprev[x] = -1;
+
+    // step t: triples of t+2 -> trX, rows of t+1 (from trY) -> rwY, apply rwX
+    auto step = [&](int t, Tri& trX, Tri& trY, Rows& rwX, Rows& rwY) __attribute__((always_inline)) {
+        load_tri(t + 2, trX);
+        unpack_gather(trY, rwY);
+        VT p[S][V], q[S][V];
+        T bu[S], bi[S];
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+            const bool fwd = uprev[x] == rwX.u[x];
+            const VT* row = reinterpret_cast<const VT*>(Qs + (size_t)rwX.i[x] * k);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const int vi = v * GS + l;
+                const bool in = vi < kv;
+                p[x][v] = in ? (fwd ? pprev[x][v] : rwX.p[x][v]) : (VT)(T)0;
+                q[x][v] = in ? row[vi] : (VT)(T)0;
+            }
+            if constexpr (KERN != MF_RBF) {
+                bu[x] = Bus[rwX.u[x] - ulo];
+                bi[x] = Bis[rwX.i[x]];
+            } else {
+                bu[x] = bi[x] = (T)0;
+            }
+        }
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+            const T sm = group_sum<GS>(lane_partial<T, W, V, KERN>(p[x], q[x]));
+            T e, d;
+            sgd_error<T, KERN>(sm, bu[x], bi[x], rwX.r[x], h, e, d);
+            const bool lead = rwX.have[x] && l == 0;
+            if constexpr (KERN != MF_RBF) {
+                if (A.upd_user && lead) Bus[rwX.u[x] - ulo] = sgd_bias<T, KERN>(bu[x], e, d, h);
+                if (A.upd_item && lead) Bis[rwX.i[x]] = sgd_bias<T, KERN>(bi[x], e, d, h);
+            }
+            VT* pw = reinterpret_cast<VT*>(A.P + (int64_t)rwX.u[x] * k);
+            VT* qw = reinterpret_cast<VT*>(Qs + (size_t)rwX.i[x] * k);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const int vi = v * GS + l;
+                VT np, nq;
+                sgd_rows<T, KERN>(p[x][v], q[x][v], e, d, h, np, nq);
+                pprev[x][v] = np;
+                if (!(rwX.have[x] && vi < kv)) continue;
+                if (A.upd_user) st<true>(pw + vi, np);
+                if (A.upd_item) qw[vi] = nq;
+            }
+            uprev[x] = (rwX.have[x] && A.upd_user) ? rwX.u[x] : -1;
+        }
+        lds_barrier();
+    };
+
+    Tri ta, tb;
+    Rows ra, rb;
+    if (nst > 0) {
+        load_tri(0, ta);
+        load_tri(1, tb);
+        unpack_gather(ta, ra);
     }
-    if (nc == 0) __syncthreads();
+    for (int t = 0; t < nst; t += 2) {
+        step(t, ta, tb, ra, rb);
+        if (t + 1 < nst) step(t + 1, tb, ta, rb, ra);
+    }
+    __syncthreads();
 
     // ---- write the slab and the bias slices back
     if (A.upd_item) {
@@ -213,13 +276,19 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata(StrataArgs<T> A) 
 
 struct StrataParams {
     const int32_t* u; const int32_t* i; const void* r;
-    const int32_t* ubnd; const int32_t* ibnd; const int64_t* boff;
-    const int32_t* cstart; const int32_t* coff;
-    int32_t B; int32_t max_items; int32_t max_users;
+    const int32_t* ubnd; const int32_t* ibnd; const int64_t* bstep;
+    int32_t B; int32_t n_slots; int32_t max_items; int32_t max_users;
     const int32_t* seq; int32_t n_seq; uint32_t seed;
     double mu; void* bu; void* bi; void* P; void* Q; int32_t k; int32_t kernel;
     double gamma, lr, reg, lo, hi; int32_t uu, ui, flags;
     hipStream_t stream; double* kernel_ms;
+};
+
+// NS of the row layout (W, GS, V) that dispatch_rows picks for (k, dtype)
+template <typename T>
+struct StrataSlots {
+    template <int W, int GS, int V, int KERN>
+    int run() { return strata_slots<T, W, GS, V>(); }
 };
 
 template <typename T>
@@ -228,17 +297,23 @@ struct StrataRun {
 
     template <int W, int GS, int V, int KERN>
     int run() {
-        // two rating slots per wave: 16 waves x 8 ratings = one 128-rating
-        // pass per colour at rank 64 (colours hold ~m/D ratings)
-        constexpr int SD = (kWave / GS) >= 8 ? 1 : 2;
-        return go<W, GS, V, KERN, SD>();
+        return go<W, GS, V, KERN, strata_group_slots<T, W, GS, V>()>();
     }
 
     template <int W, int GS, int V, int KERN, int S>
     int go() {
+        if (p.n_slots != strata_slots<T, W, GS, V>()) {
+            set_error("plan has %d slots per step, the n_factors=%d layout needs %d", p.n_slots,
+                      p.k, strata_slots<T, W, GS, V>());
+            return MF_ERR_INVALID;
+        }
         const size_t lds = strata_lds_bytes<T>(p.max_items, p.max_users, p.k);
         if (lds > (size_t)kLdsLimit) {
             set_error("strata block needs %zu B of LDS (> %d): use more blocks", lds, kLdsLimit);
+            return MF_ERR_INVALID;
+        }
+        if (p.k < 1) {
+            set_error("the strata schedule needs n_factors >= 1");
             return MF_ERR_INVALID;
         }
         auto kfn = k_sgd_strata<T, W, GS, V, KERN, S>;
@@ -248,7 +323,7 @@ struct StrataRun {
         a.u = p.u; a.i = p.i; a.r = static_cast<const T*>(p.r);
         a.P = static_cast<T*>(p.P); a.Q = static_cast<T*>(p.Q);
         a.Bu = static_cast<T*>(p.bu); a.Bi = static_cast<T*>(p.bi);
-        a.ubnd = p.ubnd; a.ibnd = p.ibnd; a.boff = p.boff; a.cstart = p.cstart; a.coff = p.coff;
+        a.ubnd = p.ubnd; a.ibnd = p.ibnd; a.bstep = p.bstep;
         a.B = p.B; a.seed = p.seed; a.k = p.k; a.upd_user = p.uu; a.upd_item = p.ui;
         a.h = make_hyper<T>(p.mu, p.lr, p.reg, p.gamma, p.lo, p.hi);
         hipEvent_t ev[2] = {nullptr, nullptr};

@@ -1,17 +1,25 @@
-// mf_strata_sched.cpp -- plan of the stratified sweep (mf_sched_strata;
-// kernel: mf_strata.hpp).
+// mf_strata_sched.cpp -- plan of the slotted stratified sweep
+// (mf_strata_plan_*; kernel: mf_strata.hpp).
 //
-// Ratings are bucketed into B*B blocks (user range x item range), stored
-// block-major with block (ub, ib) at stratum s = (ub - ib) mod B, slot w = ib,
-// and coloured inside each block: greedy, item-major, item j starting its
-// colour search at (sum of the previous items' degrees) mod D, D = the block's
-// largest item / user degree, so colours come out close to D in number and
-// even in size.  A user's ratings inside one block get colours >= user_gap
-// apart.  Blocks are coloured on worker threads (std::thread, no OpenMP
-// runtime next to torch's).
+// Ratings are bucketed into B*B blocks (user range x item range); block
+// (ub, ib) belongs to stratum s = (ub - ib) mod B, slot w = ib, and is stored
+// at s*B + w.  Inside a block:
+//   1. every user of the block is OWNED by one of NS rating slots (longest
+//      processing time first: users by falling degree onto the least loaded
+//      slot), so all of a user's ratings in the block run on one lane group,
+//      in program order -- the kernel never needs a barrier for user rows;
+//   2. the ratings are the edges of a bipartite multigraph (slot, item) and
+//      are edge-coloured with exactly D = max(largest slot load, largest item
+//      degree) colours (Koenig: alternating-path recolouring), one colour per
+//      step.  A step holds at most one rating per slot and per item.
+// The block's plan is a dense D x NS grid of rating indices (-1 = idle slot).
+// Blocks are planned on worker threads (std::thread, no OpenMP runtime next
+// to torch's).
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <functional>
+#include <queue>
 #include <thread>
 #include <vector>
 
@@ -22,89 +30,113 @@ void set_error(const char* fmt, ...);
 }
 using mf::set_error;
 
+struct mf_strata_plan {
+    int32_t B = 0;
+    int32_t NS = 0;
+    std::vector<int64_t> bstep;     // B*B + 1 step offsets
+    std::vector<int32_t> sched;     // bstep[B*B] * NS positions
+};
+
 namespace {
 
 struct Scratch {
-    std::vector<int32_t> idx, byitem, icount, ucount, uhead, next, colour, csize, cpos;
-    std::vector<uint32_t> stamp;
-    uint32_t cur = 0;
+    std::vector<int32_t> ucnt, uslot, users, load;
+    std::vector<int32_t> es, eq, ej, ecol, icnt;
+    std::vector<int32_t> sc, ic, path;
 };
 
-// Colour block [lo, hi) of `sched` in place; returns the colour offsets
-// (relative to lo, n_colours + 1 entries).
-std::vector<int32_t> colour_block(const int32_t* u, const int32_t* it, int32_t* sched, int64_t lo,
-                                  int64_t hi, int32_t ilo, int32_t nqi, int32_t ulo, int32_t nus,
-                                  int32_t gap, Scratch& S) {
-    const int32_t m = (int32_t)(hi - lo);
-    std::vector<int32_t> offs(1, 0);
-    if (m == 0) return offs;
-    S.idx.assign(sched + lo, sched + hi);
-    S.icount.assign((size_t)nqi + 1, 0);
-    if ((int32_t)S.ucount.size() < nus) S.ucount.resize(nus, 0);
-    if ((int32_t)S.uhead.size() < nus) S.uhead.resize(nus, -1);
-    int32_t dmax = 1;
+// Plan one block: ratings idx[0..m) with item ids in [ilo, ilo+nqi) and user
+// ids in [ulo, ulo+nus).  Appends D*NS entries to `grid`; returns D.
+int32_t plan_block(const int32_t* u, const int32_t* it, const int32_t* idx, int32_t m,
+                   int32_t ilo, int32_t nqi, int32_t ulo, int32_t nus, int32_t NS, Scratch& S,
+                   std::vector<int32_t>& grid) {
+    if (m == 0) return 0;
+    if ((int32_t)S.ucnt.size() < nus) {
+        S.ucnt.resize(nus, 0);
+        S.uslot.resize(nus, -1);
+    }
+    S.users.clear();
     for (int32_t x = 0; x < m; ++x) {
-        const int32_t j = S.idx[x];
-        ++S.icount[it[j] - ilo + 1];
-        dmax = std::max(dmax, ++S.ucount[u[j] - ulo]);
+        const int32_t ul = u[idx[x]] - ulo;
+        if (S.ucnt[ul]++ == 0) S.users.push_back(ul);
     }
-    for (int32_t q = 0; q < nqi; ++q) {
-        dmax = std::max(dmax, S.icount[q + 1]);
-        S.icount[q + 1] += S.icount[q];
+    // longest processing time first: users by falling degree (ties: id)
+    std::sort(S.users.begin(), S.users.end(), [&](int32_t a, int32_t b) {
+        return S.ucnt[a] != S.ucnt[b] ? S.ucnt[a] > S.ucnt[b] : a < b;
+    });
+    S.load.assign(NS, 0);
+    using LS = std::pair<int32_t, int32_t>;      // (load, slot), least first
+    std::priority_queue<LS, std::vector<LS>, std::greater<LS>> heap;
+    for (int32_t s = 0; s < NS; ++s) heap.push({0, s});
+    int32_t D = 1;
+    for (int32_t ul : S.users) {
+        LS top = heap.top();
+        heap.pop();
+        S.uslot[ul] = top.second;
+        top.first += S.ucnt[ul];
+        S.load[top.second] = top.first;
+        D = std::max(D, top.first);
+        heap.push(top);
     }
-    S.byitem.resize(m);
-    for (int32_t x = 0; x < m; ++x) {                  // stable by item
-        const int32_t j = S.idx[x];
-        S.byitem[S.icount[it[j] - ilo]++] = j;
+    S.icnt.assign(nqi, 0);
+    S.es.resize(m);
+    S.eq.resize(m);
+    S.ej.resize(m);
+    for (int32_t x = 0; x < m; ++x) {
+        const int32_t j = idx[x];
+        S.es[x] = S.uslot[u[j] - ulo];
+        S.eq[x] = it[j] - ilo;
+        S.ej[x] = j;
+        D = std::max(D, ++S.icnt[S.eq[x]]);
     }
-    for (int32_t x = 0; x < m; ++x) S.ucount[u[S.idx[x]] - ulo] = 0;
-    S.next.resize(m);
-    S.colour.resize(m);
-    const int32_t D = dmax;
-    int64_t rot = 0;
-    int32_t ncol = 0;
-    int32_t x = 0;
-    while (x < m) {
-        const int32_t item = it[S.byitem[x]];
-        int32_t y = x;
-        while (y < m && it[S.byitem[y]] == item) ++y;
-        if (++S.cur == 0) {                            // stamp wrap: reset
-            std::fill(S.stamp.begin(), S.stamp.end(), 0u);
-            S.cur = 1;
+    for (int32_t ul : S.users) {
+        S.ucnt[ul] = 0;
+        S.uslot[ul] = -1;
+    }
+    // Koenig edge colouring with D colours
+    S.sc.assign((size_t)NS * D, -1);
+    S.ic.assign((size_t)nqi * D, -1);
+    S.ecol.assign(m, -1);
+    auto set = [&](int32_t e, int32_t c) {
+        S.ecol[e] = c;
+        S.sc[(size_t)S.es[e] * D + c] = e;
+        S.ic[(size_t)S.eq[e] * D + c] = e;
+    };
+    for (int32_t e = 0; e < m; ++e) {
+        const int32_t s = S.es[e], q = S.eq[e];
+        const int32_t* scs = &S.sc[(size_t)s * D];
+        const int32_t* ics = &S.ic[(size_t)q * D];
+        int32_t a = 0, b = 0;
+        while (scs[a] >= 0) ++a;                 // free at the slot (< D: load <= D)
+        while (ics[b] >= 0) ++b;                 // free at the item
+        if (ics[a] < 0) { set(e, a); continue; }
+        if (scs[b] < 0) { set(e, b); continue; }
+        // swap a <-> b along the alternating path that leaves item q by its
+        // a-edge; it never reaches slot s (s has no a-edge), so afterwards a
+        // is free at both ends of e
+        S.path.clear();
+        int32_t cur = q;
+        for (;;) {
+            const int32_t e1 = S.ic[(size_t)cur * D + a];
+            if (e1 < 0) break;
+            S.path.push_back(e1);
+            const int32_t e2 = S.sc[(size_t)S.es[e1] * D + b];
+            if (e2 < 0) break;
+            S.path.push_back(e2);
+            cur = S.eq[e2];
         }
-        const int32_t start = (int32_t)(rot % D);
-        rot += y - x;
-        for (int32_t z = x; z < y; ++z) {
-            const int32_t j = S.byitem[z];
-            const int32_t ul = u[j] - ulo;
-            for (int32_t t = 0;; ++t) {
-                const int32_t c = t < D ? (start + t) % D : t;
-                if (c < (int32_t)S.stamp.size() && S.stamp[c] == S.cur) continue;
-                bool ok = true;
-                for (int32_t e = S.uhead[ul]; e >= 0; e = S.next[e]) {
-                    if (std::abs(S.colour[e] - c) < gap) { ok = false; break; }
-                }
-                if (!ok) continue;
-                if (c >= (int32_t)S.stamp.size()) S.stamp.resize((size_t)c + 64, 0u);
-                S.stamp[c] = S.cur;
-                S.colour[z] = c;
-                S.next[z] = S.uhead[ul];
-                S.uhead[ul] = z;
-                ncol = std::max(ncol, c + 1);
-                break;
-            }
+        for (int32_t pe : S.path) {
+            const int32_t c = S.ecol[pe];
+            S.sc[(size_t)S.es[pe] * D + c] = -1;
+            S.ic[(size_t)S.eq[pe] * D + c] = -1;
         }
-        x = y;
+        for (int32_t pe : S.path) set(pe, S.ecol[pe] == a ? b : a);
+        set(e, a);
     }
-    for (int32_t z = 0; z < m; ++z) S.uhead[u[S.byitem[z]] - ulo] = -1;
-    // stable counting sort by colour
-    S.csize.assign((size_t)ncol + 1, 0);
-    for (int32_t z = 0; z < m; ++z) ++S.csize[S.colour[z] + 1];
-    for (int32_t c = 0; c < ncol; ++c) S.csize[c + 1] += S.csize[c];
-    offs.assign(S.csize.begin(), S.csize.end());
-    S.cpos.assign(S.csize.begin(), S.csize.end() - 1);
-    for (int32_t z = 0; z < m; ++z) sched[lo + S.cpos[S.colour[z]]++] = S.byitem[z];
-    return offs;
+    const size_t g0 = grid.size();
+    grid.resize(g0 + (size_t)D * NS, -1);
+    for (int32_t e = 0; e < m; ++e) grid[g0 + (size_t)S.ecol[e] * NS + S.es[e]] = S.ej[e];
+    return D;
 }
 
 bool bounds_ok(const int32_t* b, int32_t nb, int32_t total) {
@@ -116,26 +148,25 @@ bool bounds_ok(const int32_t* b, int32_t nb, int32_t total) {
 
 }  // namespace
 
-extern "C" int mf_sched_strata(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
-                               int32_t n_users, int32_t n_items, int32_t n_blocks,
-                               const int32_t* user_bounds, const int32_t* item_bounds,
-                               int32_t user_gap, int32_t* sched_out, int64_t* block_offsets,
-                               int32_t* colour_start, int32_t* colour_offsets,
-                               int64_t colour_cap, int64_t* n_colour_offsets) {
-    if (n < 0 || n_users < 0 || n_items < 0 || n_blocks < 1 || colour_cap < 0) {
-        set_error("invalid sizes (n=%lld, n_blocks=%d)", (long long)n, n_blocks);
+extern "C" int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
+                                    int32_t n_users, int32_t n_items, int32_t n_blocks,
+                                    const int32_t* user_bounds, const int32_t* item_bounds,
+                                    int32_t n_slots, mf_strata_plan** plan_out) {
+    if (!plan_out) {
+        set_error("NULL plan_out");
+        return MF_ERR_INVALID;
+    }
+    *plan_out = nullptr;
+    if (n < 0 || n_users < 0 || n_items < 0 || n_blocks < 1 || n_slots < 1 || n_slots > 4096) {
+        set_error("invalid sizes (n=%lld, n_blocks=%d, n_slots=%d)", (long long)n, n_blocks,
+                  n_slots);
         return MF_ERR_INVALID;
     }
     if ((int64_t)n_blocks * n_blocks >= ((int64_t)1 << 31) || n > INT32_MAX) {
         set_error("n_blocks=%d / n=%lld too large", n_blocks, (long long)n);
         return MF_ERR_INVALID;
     }
-    if (user_gap < 1 || user_gap > 2) {
-        set_error("user_gap must be 1 or 2, got %d", user_gap);
-        return MF_ERR_INVALID;
-    }
-    if (!user_bounds || !item_bounds || !block_offsets || !colour_start || !n_colour_offsets ||
-        (n > 0 && (!user_ids || !item_ids || !sched_out))) {
+    if (!user_bounds || !item_bounds || (n > 0 && (!user_ids || !item_ids))) {
         set_error("NULL argument");
         return MF_ERR_INVALID;
     }
@@ -150,7 +181,7 @@ extern "C" int mf_sched_strata(const int32_t* user_ids, const int32_t* item_ids,
         for (int32_t x = item_bounds[b]; x < item_bounds[b + 1]; ++x) ib_of[x] = b;
     }
     const int64_t BB = (int64_t)B * B;
-    std::vector<int32_t> key(n);
+    std::vector<int32_t> key(n), bucket(n);
     std::vector<int64_t> pos(BB + 1, 0);
     for (int64_t j = 0; j < n; ++j) {
         const int32_t uu = user_ids[j], ii = item_ids[j];
@@ -165,24 +196,28 @@ extern "C" int mf_sched_strata(const int32_t* user_ids, const int32_t* item_ids,
         ++pos[key[j] + 1];
     }
     for (int64_t b = 0; b < BB; ++b) pos[b + 1] += pos[b];
-    std::copy(pos.begin(), pos.end(), block_offsets);
-    for (int64_t j = 0; j < n; ++j) sched_out[pos[key[j]]++] = (int32_t)j;
+    std::vector<int64_t> boff(pos);
+    for (int64_t j = 0; j < n; ++j) bucket[pos[key[j]]++] = (int32_t)j;
     std::vector<int32_t>().swap(key);
 
-    std::vector<std::vector<int32_t>> offs(BB);
+    // plan the blocks in chunks of 64 on worker threads
+    const int64_t CH = 64;
+    const int64_t nch = (BB + CH - 1) / CH;
+    std::vector<std::vector<int32_t>> grids(nch);
+    std::vector<int32_t> steps(BB, 0);
     std::atomic<int64_t> next{0};
     auto worker = [&]() {
         Scratch S;
         for (;;) {
-            const int64_t b0 = next.fetch_add(64);
-            if (b0 >= BB) break;
-            for (int64_t b = b0; b < std::min(BB, b0 + 64); ++b) {
+            const int64_t c = next.fetch_add(1);
+            if (c >= nch) break;
+            for (int64_t b = c * CH; b < std::min(BB, (c + 1) * CH); ++b) {
                 const int32_t s = (int32_t)(b / B), w = (int32_t)(b % B);
                 const int32_t ub = (w + s) % B;
-                offs[b] = colour_block(user_ids, item_ids, sched_out, block_offsets[b],
-                                       block_offsets[b + 1], item_bounds[w],
-                                       item_bounds[w + 1] - item_bounds[w], user_bounds[ub],
-                                       user_bounds[ub + 1] - user_bounds[ub], user_gap, S);
+                steps[b] = plan_block(user_ids, item_ids, bucket.data() + boff[b],
+                                      (int32_t)(boff[b + 1] - boff[b]), item_bounds[w],
+                                      item_bounds[w + 1] - item_bounds[w], user_bounds[ub],
+                                      user_bounds[ub + 1] - user_bounds[ub], n_slots, S, grids[c]);
             }
         }
     };
@@ -193,19 +228,38 @@ extern "C" int mf_sched_strata(const int32_t* user_ids, const int32_t* item_ids,
     worker();
     for (auto& t : th) t.join();
 
-    int64_t tot = 0;
-    for (int64_t b = 0; b < BB; ++b) {
-        colour_start[b] = (int32_t)tot;
-        tot += (int64_t)offs[b].size();
+    auto* plan = new (std::nothrow) mf_strata_plan;
+    if (!plan) {
+        set_error("out of host memory");
+        return MF_ERR_NOMEM;
     }
-    colour_start[BB] = (int32_t)tot;
-    *n_colour_offsets = tot;
-    if (tot > colour_cap || tot >= INT32_MAX) {
-        set_error("colour_offsets needs %lld entries, colour_cap=%lld", (long long)tot,
-                  (long long)colour_cap);
-        return MF_ERR_INVALID;
+    plan->B = B;
+    plan->NS = n_slots;
+    plan->bstep.resize(BB + 1);
+    plan->bstep[0] = 0;
+    for (int64_t b = 0; b < BB; ++b) plan->bstep[b + 1] = plan->bstep[b] + steps[b];
+    plan->sched.reserve((size_t)plan->bstep[BB] * n_slots);
+    for (auto& g : grids) {
+        plan->sched.insert(plan->sched.end(), g.begin(), g.end());
+        std::vector<int32_t>().swap(g);
     }
-    for (int64_t b = 0; b < BB; ++b)
-        std::copy(offs[b].begin(), offs[b].end(), colour_offsets + colour_start[b]);
+    *plan_out = plan;
     return MF_OK;
 }
+
+extern "C" int64_t mf_strata_plan_positions(const mf_strata_plan* plan) {
+    return plan ? (int64_t)plan->sched.size() : -1;
+}
+
+extern "C" int mf_strata_plan_fetch(const mf_strata_plan* plan, int32_t* sched_out,
+                                    int64_t* block_steps) {
+    if (!plan || !block_steps || (!plan->sched.empty() && !sched_out)) {
+        set_error("NULL argument");
+        return MF_ERR_INVALID;
+    }
+    std::copy(plan->sched.begin(), plan->sched.end(), sched_out);
+    std::copy(plan->bstep.begin(), plan->bstep.end(), block_steps);
+    return MF_OK;
+}
+
+extern "C" void mf_strata_plan_free(mf_strata_plan* plan) { delete plan; }

@@ -44,8 +44,8 @@ SIGNATURES = {
         _P, _PD]),                                    # stream kernel_ms
     "mf_sgd_workspace_bytes": (ctypes.c_size_t, [_I32]),
     "mf_sgd_epoch_strata": (ctypes.c_int, [
-        _P, _P, _P, _I64, _I32,                       # ids, ratings, n, n_blocks
-        _P, _P, _P, _P, _P, _I32, _I32,               # plan: bounds, block/colour offsets, max sizes
+        _P, _P, _P, _I64, _I32,                       # ids, ratings, n_positions, n_blocks
+        _P, _P, _P, _I32, _I32, _I32,                 # plan: bounds, block steps, slots, max sizes
         _P, _I32, ctypes.c_uint32,                    # strata_seq, n_seq, seed
         _F64, _P, _P, _P, _P,                         # mu, bu, bi, P, Q
         _I32, _I32, _I32,                             # n_users, n_items, k
@@ -54,6 +54,7 @@ SIGNATURES = {
         _P, _PD]),                                    # stream kernel_ms
     "mf_strata_lds_bytes": (ctypes.c_size_t, [_I32, _I32, _I32, _I32]),
     "mf_strata_lds_limit": (ctypes.c_int32, []),
+    "mf_strata_slots": (ctypes.c_int32, [_I32, _I32]),
     "mf_sse_workspace_bytes": (ctypes.c_size_t, [_I64]),
     "mf_sse": (ctypes.c_int, [
         _P, _P, _P, _I64, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _F64, _F64,
@@ -80,8 +81,11 @@ SIGNATURES = {
     "mf_sched_color": (ctypes.c_int, [
         _P, _P, _I64, _I32, _I32, _P, _P, _I64, _P]),
     "mf_sched_slices": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P, _P]),
-    "mf_sched_strata": (ctypes.c_int, [
-        _P, _P, _I64, _I32, _I32, _I32, _P, _P, _I32, _P, _P, _P, _P, _I64, _P]),
+    "mf_strata_plan_build": (ctypes.c_int, [
+        _P, _P, _I64, _I32, _I32, _I32, _P, _P, _I32, _P]),
+    "mf_strata_plan_positions": (_I64, [_P]),
+    "mf_strata_plan_fetch": (ctypes.c_int, [_P, _P, _P]),
+    "mf_strata_plan_free": (None, [_P]),
 }
 
 

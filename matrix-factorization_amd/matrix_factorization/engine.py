@@ -156,69 +156,87 @@ def balanced_bounds(ids: np.ndarray, m: int, n_blocks: int, by_count: bool = Tru
 
 
 class StrataPlan:
-    """Host + device form of a mf_sched_strata plan."""
+    """Host + device form of a mf_strata_plan: B x B blocks, each a grid of
+    ``n_steps`` x ``NS`` rating slots (``sched``: rating index per position,
+    -1 = idle slot)."""
 
-    def __init__(self, B, ubnd, ibnd, boff, cstart, coff, dev):
-        self.B = int(B)
-        self.ubnd, self.ibnd, self.boff, self.cstart, self.coff = ubnd, ibnd, boff, cstart, coff
+    def __init__(self, B, NS, ubnd, ibnd, bstep, sched):
+        self.B, self.NS = int(B), int(NS)
+        self.ubnd, self.ibnd, self.bstep, self.sched = ubnd, ibnd, bstep, sched
         self.max_items = int(np.diff(ibnd).max()) if B else 0
         self.max_users = int(np.diff(ubnd).max()) if B else 0
+
+    def to_device(self, u, i, r, dev) -> None:
+        """Upload the bounds, the step offsets and the triples in plan order
+        (idle slots: user -1, item -1, rating 0)."""
         to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-        self.d_ubnd, self.d_ibnd, self.d_boff = to(ubnd), to(ibnd), to(boff)
-        self.d_cstart, self.d_coff = to(cstart), to(coff)
+        self.d_ubnd, self.d_ibnd, self.d_bstep = to(self.ubnd), to(self.ibnd), to(self.bstep)
+        valid = self.sched >= 0
+        idx = np.where(valid, self.sched, 0)
+        self.d_u = to(np.where(valid, u[idx], -1).astype(np.int32))
+        self.d_i = to(np.where(valid, i[idx], -1).astype(np.int32))
+        self.d_r = to(np.where(valid, r[idx], 0).astype(r.dtype))
 
     @property
-    def n_colours(self) -> np.ndarray:
-        return np.diff(self.cstart) - 1
+    def n_positions(self) -> int:
+        return len(self.sched)
+
+    @property
+    def n_steps(self) -> np.ndarray:
+        return np.diff(self.bstep)
+
+    def stratum_sizes(self) -> np.ndarray:
+        """Ratings per stratum (launch)."""
+        cnt = np.concatenate([[0], np.cumsum(self.sched >= 0)])
+        edges = self.bstep[:: self.B] * self.NS
+        return np.diff(cnt[edges])
 
     def serial_order(self, seq, seed) -> np.ndarray:
-        """Plan positions in the order one epoch (strata ``seq``, ``seed``)
+        """Rating indices in the order one epoch (strata ``seq``, ``seed``)
         applies them: a sequential order the GPU result equals."""
-        B = self.B
+        B, NS = self.B, self.NS
         out = []
         for s in seq:
             for w in range(B):
                 blk = int(s) * B + w
-                c0 = int(self.cstart[blk])
-                nc = int(self.cstart[blk + 1]) - c0 - 1
-                if nc <= 0:
+                st0 = int(self.bstep[blk])
+                nst = int(self.bstep[blk + 1]) - st0
+                if nst <= 0:
                     continue
-                base = int(self.boff[blk])
-                rot = strata_mix(seed, blk) % nc
-                for cc in range(nc):
-                    c = (rot + cc) % nc
-                    out.append(np.arange(base + self.coff[c0 + c], base + self.coff[c0 + c + 1]))
-        return np.concatenate(out) if out else np.empty(0, np.int64)
+                rot = strata_mix(seed, blk) % nst
+                steps = (rot + np.arange(nst)) % nst
+                grid = self.sched[st0 * NS:(st0 + nst) * NS].reshape(nst, NS)[steps].ravel()
+                out.append(grid[grid >= 0])
+        return np.concatenate(out).astype(np.int64) if out else np.empty(0, np.int64)
 
 
 def sched_strata(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int, n_blocks: int,
-                 ubnd: np.ndarray, ibnd: np.ndarray, user_gap: int = 1):
-    """mf_sched_strata: (rating indices in plan order, block offsets, colour
-    starts, colour offsets)."""
+                 ubnd: np.ndarray, ibnd: np.ndarray, n_slots: int):
+    """mf_strata_plan_build + fetch: (sched, block step offsets)."""
     n = len(u)
     u = np.ascontiguousarray(u, np.int32)
     i = np.ascontiguousarray(i, np.int32)
     ubnd = np.ascontiguousarray(ubnd, np.int32)
     ibnd = np.ascontiguousarray(ibnd, np.int32)
-    BB = n_blocks * n_blocks
-    sched = np.empty(max(n, 1), np.int32)
-    boff = np.empty(BB + 1, np.int64)
-    cstart = np.empty(BB + 1, np.int32)
-    cap = max(BB * 24 + 1, 1024)
-    for _ in range(2):
-        coff = np.empty(cap, np.int32)
-        used = ctypes.c_int64(0)
-        rc = _lib.load().mf_sched_strata(_np(u), _np(i), n, n_users, n_items, n_blocks,
-                                         _np(ubnd), _np(ibnd), user_gap, _np(sched),
-                                         _np(boff), _np(cstart), _np(coff), cap,
-                                         ctypes.byref(used))
-        if rc == 0:
-            return sched[:n], boff, cstart, coff[: used.value].copy()
-        if used.value > cap:
-            cap = int(used.value)
-            continue
-        _lib.check(rc, "mf_sched_strata")
-    _lib.check(1, "mf_sched_strata")
+    lib = _lib.load()
+    handle = ctypes.c_void_p()
+    _lib.call("mf_strata_plan_build", _np(u), _np(i), n, n_users, n_items, n_blocks,
+              _np(ubnd), _np(ibnd), n_slots, ctypes.byref(handle))
+    try:
+        npos = int(lib.mf_strata_plan_positions(handle))
+        sched = np.empty(max(npos, 1), np.int32)
+        bstep = np.empty(n_blocks * n_blocks + 1, np.int64)
+        _lib.call("mf_strata_plan_fetch", handle, _np(sched), _np(bstep))
+    finally:
+        lib.mf_strata_plan_free(handle)
+    return sched[:npos], bstep
+
+
+def strata_slots(k: int, dcode: int) -> int:
+    ns = int(_lib.load().mf_strata_slots(k, dcode))
+    if ns <= 0:
+        _lib.check(1, "mf_strata_slots")
+    return ns
 
 
 def choose_strata_blocks(u, i, n_users, n_items, k, dcode, max_blocks=None):
@@ -368,9 +386,10 @@ class SGDEngine:
         self.colored = offs
         return len(offs) - 1
 
-    def prepare_strata(self, n_blocks: Optional[int] = None, user_gap: int = 1) -> "StrataPlan":
-        """Build the stratified plan once and store the ratings in plan order
-        (block-major, colour-major inside a block)."""
+    def prepare_strata(self, n_blocks: Optional[int] = None) -> "StrataPlan":
+        """Build the stratified plan once and store a padded copy of the
+        ratings in plan order (block-major, step-major, slot-minor).  The
+        host arrays keep the original rating order."""
         if self.colored is not None or self.strata is not None:
             raise RuntimeError("ratings already permuted by another schedule")
         if n_blocks is None:
@@ -380,14 +399,13 @@ class SGDEngine:
             B = int(n_blocks)
             ub = balanced_bounds(self.u_host, self.n_users, B)
             ib = balanced_bounds(self.i_host, self.n_items, B)
-        sched, boff, cstart, coff = sched_strata(self.u_host, self.i_host, self.n_users,
-                                                 self.n_items, B, ub, ib, user_gap)
-        self.u_host = self.u_host[sched]
-        self.i_host = self.i_host[sched]
-        self.r_host = self.r_host[sched]
-        self._upload_triples(self.u_host, self.i_host, self.r_host)
-        self.strata = StrataPlan(B, ub, ib, boff, cstart, coff, self.dev)
-        return self.strata
+        ns = strata_slots(self.k, self.dcode)
+        sched, bstep = sched_strata(self.u_host, self.i_host, self.n_users, self.n_items, B,
+                                    ub, ib, ns)
+        plan = StrataPlan(B, ns, ub, ib, bstep, sched)
+        plan.to_device(self.u_host, self.i_host, self.r_host, self.dev)
+        self.strata = plan
+        return plan
 
     def epoch_strata(self, seq: Optional[np.ndarray], seed: int, lr: float, reg: float,
                      update_user: bool = True, update_item: bool = True, timing=False):
@@ -400,9 +418,9 @@ class SGDEngine:
                else np.ascontiguousarray(seq, np.int32))
         ms = (ctypes.c_double * 2)() if timing else None
         with torch.cuda.device(self.dev):
-            _lib.call("mf_sgd_epoch_strata", _tp(self.u), _tp(self.i), _tp(self.r), self.n,
-                      pl.B, _tp(pl.d_ubnd), _tp(pl.d_ibnd), _tp(pl.d_boff), _tp(pl.d_cstart),
-                      _tp(pl.d_coff), pl.max_items, pl.max_users, _np(seq), len(seq),
+            _lib.call("mf_sgd_epoch_strata", _tp(pl.d_u), _tp(pl.d_i), _tp(pl.d_r),
+                      pl.n_positions, pl.B, _tp(pl.d_ubnd), _tp(pl.d_ibnd), _tp(pl.d_bstep),
+                      pl.NS, pl.max_items, pl.max_users, _np(seq), len(seq),
                       int(seed) & 0xFFFFFFFF, self.global_mean, _tp(self.bu), _tp(self.bi),
                       _tp(self.P), _tp(self.Q), self.n_users, self.n_items, self.k,
                       self.kcode, self.dcode, self.gamma, float(lr), float(reg),

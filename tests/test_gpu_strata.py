@@ -1,13 +1,14 @@
 """GPU parity of the stratified sweep (schedule='strata', mf_strata.hpp).
 
 A strata epoch applies the ratings in one sequential order (strata in the
-given order, blocks of a stratum in any order, colours of a block from the
+given order, blocks of a stratum in any order, steps of a block from the
 seeded rotation); StrataPlan.serial_order lists it.  The GPU result must equal
 the oracle's sequential sweep over that order:
   FP64 parameters: max |diff| <= 1e-11 * max(1, |value|), RMSE <= 1e-12
   FP32 state vs FP64 oracle: RMSE <= 1e-5 (the north-star bar)
-Every block holds several ratings per user, spread over different colours, so
-the colour barrier's ordering of user-row stores and loads is exercised.
+Every block holds several ratings per user on the user's slot, often in
+consecutive steps, so both the prefetched user rows (read before the previous
+step's stores) and the forwarding of a just-updated row are exercised.
 """
 
 import numpy as np
@@ -45,10 +46,9 @@ def _engine(u, i, r, nu, ni, k, kernel, dtype, P, Q, bu, bi):
 
 
 # FP64 LDS image per block: items/B * (k+1) * 8 B + users/B * 8 B <= 160 KiB
-@pytest.mark.parametrize("kernel,k,B,gap", [("linear", 64, 4, 1), ("sigmoid", 32, 3, 2),
-                                            ("rbf", 16, 5, 1), ("linear", 100, 8, 1),
-                                            ("sigmoid", 7, 2, 1), ("linear", 8, 1, 1)])
-def test_strata_epochs_equal_serialized_oracle(kernel, k, B, gap):
+@pytest.mark.parametrize("kernel,k,B", [("linear", 64, 4), ("sigmoid", 32, 3), ("rbf", 16, 5),
+                                        ("linear", 100, 8), ("sigmoid", 7, 2), ("linear", 8, 1)])
+def test_strata_epochs_equal_serialized_oracle(kernel, k, B):
     import oracle
 
     nu, ni, nnz = 3000, 800, 120000
@@ -57,7 +57,7 @@ def test_strata_epochs_equal_serialized_oracle(kernel, k, B, gap):
     P = rs.normal(0, 0.1, (nu, k)); Q = rs.normal(0, 0.1, (ni, k))
     bu = np.zeros(nu); bi = np.zeros(ni)
     eng = _engine(u, i, r, nu, ni, k, kernel, "float64", P, Q, bu, bi)
-    plan = eng.prepare_strata(n_blocks=B, user_gap=gap)
+    plan = eng.prepare_strata(n_blocks=B)
     assert plan.B == B
     mu = eng.global_mean
     hyp = dict(kernel=kernel, gamma=eng.gamma, min_rating=1.0, max_rating=5.0)

@@ -363,11 +363,12 @@ def test_slice_order_groups_items_then_users():
 
 
 # ------------------------------------------------------------ strata plan
-@pytest.mark.parametrize("B,gap", [(1, 1), (3, 2), (8, 1)])
-def test_strata_plan_is_valid(B, gap):
-    """mf_sched_strata: a permutation; block (s, w) holds user range (w+s)%B
-    x item range w; every colour is a matching; user colours >= gap apart;
-    colour counts reach the largest degree inside the block (B = 1)."""
+@pytest.mark.parametrize("B,NS", [(1, 32), (3, 16), (8, 128)])
+def test_strata_plan_is_valid(B, NS):
+    """mf_strata_plan_build: every rating placed once; block (s, w) holds user
+    range (w+s)%B x item range w; a step holds each slot and each item at most
+    once; every user of a block stays on one slot; the block has exactly
+    D = max(slot load, item degree) steps (Koenig colouring)."""
     from matrix_factorization import engine as E
 
     rs = np.random.RandomState(0)
@@ -377,29 +378,35 @@ def test_strata_plan_is_valid(B, gap):
     i = (keys % ni).astype(np.int32)
     ub = E.balanced_bounds(u, nu, B)
     ib = E.balanced_bounds(i, ni, B)
-    sched, boff, cst, coff = E.sched_strata(u, i, nu, ni, B, ub, ib, gap)
-    assert np.array_equal(np.sort(sched), np.arange(n))
-    us, is_ = u[sched], i[sched]
+    sched, bstep = E.sched_strata(u, i, nu, ni, B, ub, ib, NS)
+    assert len(sched) == bstep[-1] * NS
+    valid = sched[sched >= 0]
+    assert np.array_equal(np.sort(valid), np.arange(n))
     for s in range(B):
         for w in range(B):
             blk = s * B + w
-            lo, hi = boff[blk], boff[blk + 1]
+            nst = bstep[blk + 1] - bstep[blk]
+            grid = sched[bstep[blk] * NS:bstep[blk + 1] * NS].reshape(nst, NS)
             ubk = (w + s) % B
-            assert np.all((us[lo:hi] >= ub[ubk]) & (us[lo:hi] < ub[ubk + 1]))
-            assert np.all((is_[lo:hi] >= ib[w]) & (is_[lo:hi] < ib[w + 1]))
-            c0, nc = cst[blk], cst[blk + 1] - cst[blk] - 1
-            offs = coff[c0:c0 + nc + 1]
-            assert offs[0] == 0 and offs[-1] == hi - lo and np.all(np.diff(offs) >= 0)
-            col = np.repeat(np.arange(nc), np.diff(offs))
-            for c in range(nc):
-                a, b = lo + offs[c], lo + offs[c + 1]
-                assert len(set(us[a:b])) == b - a and len(set(is_[a:b])) == b - a
-            order = np.lexsort((col, us[lo:hi]))
-            same = np.diff(us[lo:hi][order]) == 0
-            assert np.all(np.diff(col[order])[same] >= gap)
-    if B == 1:
-        dmax = max(np.bincount(u).max(), np.bincount(i).max())
-        assert cst[1] - 1 == dmax
+            js = grid[grid >= 0]
+            assert np.all((u[js] >= ub[ubk]) & (u[js] < ub[ubk + 1]))
+            assert np.all((i[js] >= ib[w]) & (i[js] < ib[w + 1]))
+            owner = {}
+            load = np.zeros(NS, np.int64)
+            for t in range(nst):
+                row = grid[t]
+                on = row >= 0
+                items = i[row[on]]
+                assert len(set(items)) == len(items)          # item once per step
+                for slot in np.nonzero(on)[0]:
+                    user = int(u[row[slot]])
+                    assert owner.setdefault(user, slot) == slot   # one slot per user
+                    load[slot] += 1
+            if len(js):
+                D = max(load.max(), np.bincount(i[js]).max())
+                assert nst == D
+            else:
+                assert nst == 0
 
 
 def test_strata_serial_order_and_rejections():
@@ -410,15 +417,22 @@ def test_strata_serial_order_and_rejections():
     i = np.array([0, 1, 1, 0, 2, 2], np.int32)
     ub = np.array([0, 2, 4], np.int32)
     ib = np.array([0, 1, 3], np.int32)
-    sched, boff, cst, coff = E.sched_strata(u, i, 4, 3, 2, ub, ib)
-    plan = E.StrataPlan.__new__(E.StrataPlan)
-    plan.B, plan.boff, plan.cstart, plan.coff = 2, boff, cst, coff
+    sched, bstep = E.sched_strata(u, i, 4, 3, 2, ub, ib, 4)
+    plan = E.StrataPlan(2, 4, ub, ib, bstep, sched)
     order = plan.serial_order([1, 0], 12345)
     assert np.array_equal(np.sort(order), np.arange(6))
-    # stratum 1 first: its positions come before stratum 0's
-    assert set(order[: boff[4] - boff[2]]) == set(range(boff[2], boff[4]))
+    # stratum 1 first: its ratings come before stratum 0's
+    sizes = plan.stratum_sizes()
+    assert sizes.sum() == 6
+    s1 = sched[bstep[2] * 4:bstep[4] * 4]
+    assert set(order[: sizes[1]]) == set(s1[s1 >= 0])
     with pytest.raises(_lib.MFLibraryError):
-        E.sched_strata(u, i, 4, 3, 2, np.array([0, 3, 2], np.int32), ib)
+        E.sched_strata(u, i, 4, 3, 2, np.array([0, 3, 2], np.int32), ib, 4)
     with pytest.raises(_lib.MFLibraryError):
-        E.sched_strata(u, i, 4, 3, 2, ub, ib, user_gap=3)
+        E.sched_strata(u, i, 4, 3, 2, ub, ib, 0)
     assert E.strata_mix(0, 0) == 0 and E.strata_mix(1, 2) != E.strata_mix(2, 1)
+    # slots per step follow the kernel's row layout
+    assert E.strata_slots(64, _lib.MF_F32) == 128
+    assert E.strata_slots(16, _lib.MF_F32) == 256
+    assert E.strata_slots(64, _lib.MF_F64) == 64          # one slot per group (FP64 rows)
+    assert _lib.load().mf_strata_slots(-1, 0) == -1

@@ -46,6 +46,8 @@ def main():
     ap.add_argument("--bench-fetch", required=True)
     ap.add_argument("--bench-write", required=True)
     ap.add_argument("--key", default="c3/n1")
+    ap.add_argument("--sgd-kernel", default="k_sgd_batch",
+                    help="name fragment of the SGD kernel (k_sgd_batch | k_sgd_strata)")
     ap.add_argument("--out", default="profiles/traffic.json")
     ap.add_argument("--shape", default="x4", choices=["x1", "x4"],
                     help="calibration kernels matching the bench kernels' access "
@@ -59,7 +61,7 @@ def main():
     cf = known / (f_tot / f_n * 1024.0)
     cw = known / (w_tot / w_n * 1024.0)
     res = {}
-    for name, needle in (("sgd", "k_sgd_batch"), ("sse", "k_sse_stream")):
+    for name, needle in (("sgd", args.sgd_kernel), ("sse", "k_sse_stream")):
         bf, nf = pick(per_kernel(args.bench_fetch, "FETCH_SIZE"), needle)
         bw, nw = pick(per_kernel(args.bench_write, "WRITE_SIZE"), needle)
         res[name] = {
