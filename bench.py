@@ -55,6 +55,10 @@ WORKLOADS = {
            "synthetic 100Kx10K 5M-nnz rank-32 sigmoid SGD"),
     "small": (100_000, 20_000, 4_000_000, 64, "linear",
               "synthetic 100Kx20K 4M-nnz rank-64 linear SGD (smoke)"),
+    "c5": (1_000_000, 100_000, 100_000_000, 128, "als",
+           "synthetic 1Mx100K 100M-nnz rank-128 ALS (MFMA Gramian)"),
+    "c5_small": (100_000, 10_000, 5_000_000, 128, "als",
+                 "synthetic 100Kx10K 5M-nnz rank-128 ALS (smoke)"),
     # probes (not bench lines): P that fits the 256 MiB Infinity Cache
     "c3_u250k": (250_000, 100_000, 100_000_000, 64, "linear",
                  "probe: synthetic 250Kx100K 100M-nnz rank-64 linear SGD"),
@@ -101,6 +105,128 @@ def traffic_from_profiles(workload: str, n_gpus: int, schedule: str = "colored")
         return None
 
 
+MFMA_F32_PEAK_TFS = 157.3      # MI355X dense f32-input MFMA (MI355X_MICROARCH.md)
+
+
+def run_als(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
+    """BASELINE configs[4]: rank-k factor ALS (mf_als_sweep), one step = one
+    epoch = user half-sweep + item half-sweep + training-RMSE pass.
+
+    roofline: MFMA-bound.  Algorithmic flops per epoch: the
+    Gramian 2k^2 and the right-hand side 2k per rating per half-sweep, plus
+    k^3/3 per solved entity; achieved = those flops / ALS-kernel time."""
+    import torch
+
+    from matrix_factorization.engine import FactorALS, SGDEngine
+
+    if args.dtype != "float32":
+        raise SystemExit("the ALS path is float32 (f32-input MFMA Gramian)")
+    reg = 1.0 if args.reg is None else args.reg
+    eng = SGDEngine(u, i, r, nu, ni, k, "linear", "float32", dev, min_rating=1.0,
+                    max_rating=5.0, global_mean=mu)
+    t0 = time.time()
+    als = FactorALS(eng)
+    log(f"ALS CSR lists in {time.time() - t0:.1f}s")
+
+    def reset():
+        eng.load_params(P=P0, Q=Q0, bu=np.zeros(nu), bi=np.zeros(ni))
+
+    # ---- CPU baseline + parity: the user half-sweep for a prefix of users
+    cpu_baseline = parity = None
+    if args.cpu_sample > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # test infrastructure: checker and reported baseline only
+
+        deg = np.bincount(u, minlength=nu)
+        n_s = int(np.searchsorted(np.cumsum(deg), min(args.cpu_sample, 1_000_000, nnz))) + 1
+        n_s = min(n_s, nu)
+        sel = u < n_s
+        reset()
+        als.sweep_users(reg)
+        Pg, _, bug, _ = eng.params_numpy()
+        S = int(sel.sum())
+        log(f"cpu oracle: user half-sweep of {n_s} users = {S} ratings, FP64, 1 thread")
+        from threadpoolctl import threadpool_limits
+
+        with threadpool_limits(1):                 # one core, as the SGD leg
+            t0 = time.perf_counter()
+            bo, Po = oracle.als_half_sweep(u[sel], i[sel], r[sel], np.float32(mu),
+                                           np.zeros(ni), Q0, n_s, reg)
+            t_cpu = time.perf_counter() - t0
+        cpu_baseline = {
+            "value": S / t_cpu / 2, "unit": "rating-updates/s", "cores": 1, "kind": "port",
+            "sample": (f"user half-sweep of the first {n_s} users ({S} ratings, {t_cpu:.1f}s) "
+                       f"of the same workload, oracle.als_half_sweep (NumPy FP64, "
+                       f"np.linalg.solve per user); value = ratings / (2 x time), an "
+                       f"epoch being two half-sweeps"),
+        }
+        rel = np.abs(Pg[:n_s] - Po) / np.maximum(1.0, np.abs(Po))
+        parity = {"what": "user half-sweep from the same state, GPU f32 MFMA vs oracle f64",
+                  "max_rel_dP": float(rel.max()),
+                  "max_abs_dbu": float(np.max(np.abs(bug[:n_s] - bo)))}
+        log(f"cpu {cpu_baseline['value'] / 1e6:.3f} M/s; parity max rel dP "
+            f"{parity['max_rel_dP']:.2e}")
+
+    reset()
+    events = []
+
+    def epoch(ep, timed):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
+        if ev:
+            ev[0].record()
+        als.sweep_users(reg)
+        if ev:
+            ev[1].record()
+        als.sweep_items(reg)
+        if ev:
+            ev[2].record()
+        eng.sse_async(ep)
+        if ev:
+            ev[3].record()
+            events.append(ev)
+
+    for ep in range(args.warmup):
+        epoch(ep, False)
+        log(f"warmup epoch {ep + 1}/{args.warmup}")
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for j in range(args.steps):
+        epoch(args.warmup + j, not args.no_phase_timing)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    rmse = eng.rmse_values(args.warmup + args.steps)
+    roofline = phases = None
+    if events:
+        us = sum(e[0].elapsed_time(e[1]) for e in events) / 1e3
+        it = sum(e[1].elapsed_time(e[2]) for e in events) / 1e3
+        ss = sum(e[2].elapsed_time(e[3]) for e in events) / 1e3
+        flops_epoch = 2 * nnz * (2 * k * k + 2 * k) + (nu + ni) * k ** 3 / 3
+        achieved = flops_epoch * len(events) / (us + it) / 1e12
+        roofline = {"bound": "mfma", "achieved": achieved, "peak": MFMA_F32_PEAK_TFS,
+                    "unit": "TFLOP/s", "frac": achieved / MFMA_F32_PEAK_TFS, "traffic": None,
+                    "kernel": "k_als_solve", "launches": 2 * len(events),
+                    "avg_launch_us": (us + it) / (2 * len(events)) * 1e6,
+                    "flops_per_epoch": flops_epoch,
+                    "note": "f32-input MFMA peak (no xf32 on gfx950); flops = 2k^2 + 2k "
+                            "per rating per half-sweep + k^3/3 per entity"}
+        phases = {"user_sweep_ms": us / len(events) * 1e3,
+                  "item_sweep_ms": it / len(events) * 1e3,
+                  "rmse_ms": ss / len(events) * 1e3}
+    out = {
+        "metric": METRIC, "value": nnz * args.steps / elapsed, "unit": "rating-updates/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": desc, "n_users": nu, "n_items": ni, "nnz": nnz,
+                   "n_factors": k, "reg": reg, "parallelism": "single GPU",
+                   "step": "one ALS epoch: user half-sweep + item half-sweep + training RMSE"},
+        "final_rmse": rmse[-1], "rmse_per_epoch": rmse, "roofline": roofline,
+        "phases": phases, "cpu_baseline": cpu_baseline, "parity": parity,
+    }
+    print(json.dumps(out), flush=True)
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,7 +235,9 @@ def main() -> int:
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--dtype", default="float32", choices=["float32", "float64"])
     ap.add_argument("--lr", type=float, default=0.01)
-    ap.add_argument("--reg", type=float, default=0.02)
+    ap.add_argument("--reg", type=float, default=None,
+                    help="default 0.02 for SGD (project_template/pipeline/train.py:29-36), "
+                         "1.0 for ALS (KernelMF's default reg)")
     ap.add_argument("--cpu-sample", type=int, default=10_000_000,
                     help="ratings in the CPU-oracle sample (0 = skip the CPU leg)")
     ap.add_argument("--no-phase-timing", action="store_true",
@@ -146,6 +274,12 @@ def main() -> int:
     rs = np.random.RandomState(7)
     P0 = rs.normal(0.0, 0.1, (nu, k)).astype(args.dtype)
     Q0 = rs.normal(0.0, 0.1, (ni, k)).astype(args.dtype)
+    if kernel == "als":
+        if world > 1:
+            raise SystemExit("the ALS workload (configs[4]) is a single-GPU config")
+        return run_als(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev)
+    if args.reg is None:
+        args.reg = 0.02
 
     if world > 1:
         bounds = shard_users(u, nu, world)

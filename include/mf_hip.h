@@ -256,6 +256,36 @@ int mf_bias_predict(const int32_t* user_ids, const int32_t* item_ids,
                     int32_t dtype, double min_rating, double max_rating,
                     int32_t bound_ratings, void* out, void* stream);
 
+/* ---------------- factor-model ALS (BASELINE config 5) ------------------ */
+
+/*
+ * One half-sweep of alternating least squares for the factor model: solves,
+ * for every entity e (users with the item side fixed, or items with the user
+ * side fixed), the regularised normal equations of its factor row and bias
+ *     (sum_n y_n y_n^T + reg I) [w_e; b_e] = sum_n t_n y_n,
+ *     y_n = [other_features[o_n]; 1],  t_n = r_n - global_mean - other_biases[o_n]
+ * No reference counterpart: it extends the bias-only ALS of
+ * baseline_model.py:283-362 (`_als`, whose per-entity update
+ * (reg + n_e) b_e = sum t_n, :328-337, is the k = 0 case) to the latent
+ * factors of KernelMF's linear kernel.
+ *   entity_ptr      DEVICE, n_entities + 1 (int64): CSR offsets
+ *   other_ids       DEVICE, the other side's id per rating, CSR order
+ *   ratings         DEVICE, float, CSR order
+ *   other_biases / other_features   DEVICE, float, (n_other) / (n_other, k)
+ *   biases / features               DEVICE, float, written: (n_entities) /
+ *                                   (n_entities, k)
+ * Entities without ratings keep their parameters (update_users re-solves
+ * only the users present in its data).  The Gramian runs on f32-input MFMA
+ * (v_mfma_f32_32x32x2_f32), the solve is an LDS elimination in f32.  dtype must be MF_F32; 1 <= n_factors <=
+ * mf_als_max_factors().
+ */
+int mf_als_sweep(const int64_t* entity_ptr, const int32_t* other_ids,
+                 const void* ratings, int32_t n_entities, double global_mean,
+                 const void* other_biases, const void* other_features,
+                 void* biases, void* features, int32_t n_factors, int32_t dtype,
+                 double reg, void* stream);
+int32_t mf_als_max_factors(void);
+
 /* ---------------- multi-GPU replica exchange ----------------------------- */
 
 /*

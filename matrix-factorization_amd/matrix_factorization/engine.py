@@ -588,6 +588,55 @@ class BiasALS:
                       e.stream)
 
 
+class FactorALS:
+    """Alternating least squares for the factor model (BASELINE config 5;
+    mf_als_sweep): CSR lists by user and by item in HBM, one half-sweep per
+    side.  Extends the bias ALS (baseline_model.py:283-362) to the latent
+    factors; the engine must hold float32 linear-kernel parameters."""
+
+    def __init__(self, engine: SGDEngine):
+        e = engine
+        if e.dtype != "float32" or e.kernel != "linear":
+            raise ValueError("factor ALS runs on float32 linear-kernel parameters")
+        kmax = _lib.load().mf_als_max_factors()
+        if not 1 <= e.k <= kmax:
+            raise ValueError(f"factor ALS needs 1 <= n_factors <= {kmax}, got {e.k}")
+        r = e.r_host.astype(np.float32)
+
+        def csr(ent, oth, m):
+            order = np.argsort(ent, kind="stable")
+            ptr = np.zeros(m + 1, np.int64)
+            np.cumsum(np.bincount(ent, minlength=m), out=ptr[1:])
+            to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(e.dev)  # noqa: E731
+            return to(ptr), to(oth[order].astype(np.int32)), to(r[order])
+
+        self.e = e
+        self.user_csr = csr(e.u_host, e.i_host, e.n_users)
+        self.item_csr = csr(e.i_host, e.u_host, e.n_items)
+
+    def _sweep(self, csr, n, ob, oq, b, q, reg):
+        e = self.e
+        ptr, oth, rr = csr
+        with torch.cuda.device(e.dev):
+            _lib.call("mf_als_sweep", _tp(ptr), _tp(oth), _tp(rr), n, e.global_mean, _tp(ob),
+                      _tp(oq), _tp(b), _tp(q), e.k, e.dcode, float(reg), e.stream)
+
+    def sweep_users(self, reg: float) -> None:
+        """User rows and biases from the current item side."""
+        e = self.e
+        self._sweep(self.user_csr, e.n_users, e.bi, e.Q, e.bu, e.P, reg)
+
+    def sweep_items(self, reg: float) -> None:
+        """Item rows and biases from the current user side."""
+        e = self.e
+        self._sweep(self.item_csr, e.n_items, e.bu, e.P, e.bi, e.Q, reg)
+
+    def epoch(self, reg: float) -> None:
+        """Users, then items (the order of baseline_model.py:326-348)."""
+        self.sweep_users(reg)
+        self.sweep_items(reg)
+
+
 def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
                reg: float, update_user: bool = True, update_item: bool = True,
                verbose: int = 0, rng_order: Optional[np.ndarray] = None,

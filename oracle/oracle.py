@@ -153,6 +153,56 @@ def bias_als_epoch(u, i, r, mu, bu, bi, ucnt, icnt, reg):
                                 len(bu), len(bi), float(reg))
 
 
+# ------------------------------------------------------------ factor ALS
+def als_half_sweep(ent, oth, r, mu, ob, oq, n_ent, reg):
+    """Factor-model ALS, one side, FP64 (the restatement mf_als_sweep is
+    checked against; BASELINE config 5 has no reference counterpart).
+
+    For each entity e: x_e = [w_e; b_e] solves
+        (sum_n y_n y_n^T + reg I) x_e = sum_n t_n y_n,
+        y_n = [oq[oth_n]; 1],  t_n = r_n - mu - ob[oth_n],
+    the latent-factor extension of baseline_model.py:328-337 (with k = 0 it
+    is (reg + n_e) b_e = sum_n t_n exactly).  Returns (biases, rows)."""
+    ent = np.asarray(ent, np.int64)
+    oth = np.asarray(oth, np.int64)
+    r = np.asarray(r, np.float64)
+    oq = np.asarray(oq, np.float64)
+    ob = np.asarray(ob, np.float64)
+    k = oq.shape[1]
+    order = np.argsort(ent, kind="stable")
+    ptr = np.zeros(n_ent + 1, np.int64)
+    np.cumsum(np.bincount(ent, minlength=n_ent), out=ptr[1:])
+    bias = np.zeros(n_ent)
+    feat = np.zeros((n_ent, k))
+    eye = reg * np.eye(k + 1)
+    for e in range(n_ent):
+        idx = order[ptr[e]:ptr[e + 1]]
+        Y = np.empty((len(idx), k + 1))
+        Y[:, :k] = oq[oth[idx]]
+        Y[:, k] = 1.0
+        t = (r[idx] - mu) - ob[oth[idx]]
+        x = np.linalg.solve(Y.T @ Y + eye, Y.T @ t)
+        feat[e] = x[:k]
+        bias[e] = x[k]
+    return bias, feat
+
+
+def als_epoch(u, i, r, mu, bu, bi, P, Q, reg):
+    """One factor-ALS epoch as baseline_model.py:326-348 orders the bias
+    model's: users from the current item side, then items from the new user
+    side.  Returns (bu, bi, P, Q) (new arrays)."""
+    bu, P = als_half_sweep(u, i, r, mu, bi, Q, len(bu), reg)
+    bi, Q = als_half_sweep(i, u, r, mu, bu, P, len(bi), reg)
+    return bu, bi, P, Q
+
+
+def linear_rmse(u, i, r, mu, bu, bi, P, Q) -> float:
+    """Training RMSE of the linear predictor ((mu + b_i) + b_u) + p.q
+    (kernels.py:42-44, kernel_matrix_factorization.py:271-315), NumPy."""
+    pred = ((mu + bi[i]) + bu[u]) + np.einsum("nk,nk->n", P[u], Q[i])
+    return float(np.sqrt(np.mean((np.asarray(r, np.float64) - pred) ** 2)))
+
+
 # ------------------------------------------------------------ host side
 def preprocess_fit(X: pd.DataFrame, y) -> tuple:
     """recommender_base.py:120-164 for type='fit'.
