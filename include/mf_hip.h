@@ -285,6 +285,15 @@ int mf_als_sweep(const int64_t* entity_ptr, const int32_t* other_ids,
                  void* biases, void* features, int32_t n_factors, int32_t dtype,
                  double reg, void* stream);
 int32_t mf_als_max_factors(void);
+/* Profiling probe: mf_als_sweep that also writes 4 wall-clock stamps
+ * (s_memrealtime, 100 MHz) per entity to probe[4 * n_entities] (DEVICE):
+ * start, Gramian done, elimination done, end (entities without ratings:
+ * untouched). */
+int mf_als_sweep_probe(const int64_t* entity_ptr, const int32_t* other_ids,
+                       const void* ratings, int32_t n_entities, double global_mean,
+                       const void* other_biases, const void* other_features,
+                       void* biases, void* features, int32_t n_factors, int32_t dtype,
+                       double reg, void* stream, int64_t* probe);
 
 /* ---------------- multi-GPU replica exchange ----------------------------- */
 

@@ -13,11 +13,12 @@
 // k = 0 it is baseline_model.py:328-337 ((reg + n) b_e = sum t_n).
 //
 // One workgroup (4 waves) per entity:
-//   1. the Gramian [sum z z^T | sum t z | sum z] on MFMA: the entity's other-
-//      side rows are gathered in chunks of 64 into LDS and consumed by
-//      v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation), only
-//      the upper 32x32 tiles of the symmetric Gramian plus one tile column
-//      for the two right-hand columns, tiles spread over the 4 waves;
+//   1. the Gramian sum z z^T on MFMA: the entity's other-side rows are
+//      gathered in chunks of 64 into LDS (software-pipelined through
+//      registers) and consumed by v_mfma_f32_32x32x2_f32 (exact f32 products,
+//      f32 accumulation), only the upper 32x32 tiles of the symmetric
+//      Gramian, spread over the 4 waves; the right-hand columns sum t z and
+//      sum z on the VALU beside them;
 //   2. the tiles go to LDS as the upper triangle of the (KP) x (KP + 2)
 //      augmented matrix; symmetric Gaussian elimination (A = U^T D U, no
 //      pivoting: A is SPD) with one barrier per pivot row;
@@ -36,21 +37,22 @@ constexpr int kAlsMaxFactors = 128;
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-// Tiles of the Gramian: column blocks J = 0..NT (J == NT: the [t, 1] block),
-// row blocks I <= J (I < NT).  Tile q is computed by wave q % 4.
+// MFMA tiles of the symmetric Gramian: column blocks J = 0..NT-1, row blocks
+// I <= J.  Tile q is computed by wave q % 4.  The two right-hand columns
+// (sum t z, sum z) are VALU sums: wave w < NT accumulates column block w.
 template <int NT>
 struct AlsTiles {
-    static constexpr int count = NT * (NT + 1) / 2 + NT;
+    static constexpr int count = NT * (NT + 1) / 2;
     static constexpr int per_wave = (count + 3) / 4;
     static constexpr int I(int q) {
-        for (int J = 0, n = 0; J <= NT; ++J)
-            for (int i = 0; i <= (J < NT ? J : NT - 1); ++i, ++n)
+        for (int J = 0, n = 0; J < NT; ++J)
+            for (int i = 0; i <= J; ++i, ++n)
                 if (n == q) return i;
         return 0;
     }
     static constexpr int J(int q) {
-        for (int J = 0, n = 0; J <= NT; ++J)
-            for (int i = 0; i <= (J < NT ? J : NT - 1); ++i, ++n)
+        for (int J = 0, n = 0; J < NT; ++J)
+            for (int i = 0; i <= J; ++i, ++n)
                 if (n == q) return J;
         return 0;
     }
@@ -67,34 +69,45 @@ struct AlsArgs {
     int32_t k;
     float mu;
     float reg;
+    int64_t* probe;            // nullable: 4 wall-clock stamps per workgroup
 };
 
-// One K-step (two chunk rows) of wave WV: the MFMAs of its tiles.
+// profiling probe: s_memrealtime (100 MHz) at the phase boundaries
+__device__ __forceinline__ void als_stamp(const AlsArgs& A, int slot) {
+    if (A.probe && threadIdx.x == 0)
+        A.probe[(int64_t)blockIdx.x * 4 + slot] = (int64_t)__builtin_amdgcn_s_memrealtime();
+}
+
+// One K-step (two chunk rows) of wave WV: the MFMAs of its tiles, and the
+// right-hand sums of column block WV (lane (r, h): column 32 WV + r, row h).
 template <int NT, int WV>
-__device__ __forceinline__ void als_kstep(const float* zr, float tv, float ov, int r,
-                                          f32x16 (&acc)[AlsTiles<NT>::per_wave]) {
+__device__ __forceinline__ void als_kstep(const float* zr, float tv, int r,
+                                          f32x16 (&acc)[AlsTiles<NT>::per_wave],
+                                          float& fsum, float& ssum) {
     using TL = AlsTiles<NT>;
     float zv[NT];
 #pragma unroll
     for (int I = 0; I < NT; ++I) zv[I] = zr[32 * I + r];
-    const float ext = r == 0 ? tv : (r == 1 ? ov : 0.f);
 #pragma unroll
     for (int s = 0; s < TL::per_wave; ++s) {
         const int q = WV + 4 * s;
-        if (q < TL::count) {
-            const float a = zv[TL::I(q)];
-            const float b = TL::J(q) < NT ? zv[TL::J(q)] : ext;
-            acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc[s], 0, 0, 0);
-        }
+        if (q < TL::count)
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x2f32(zv[TL::I(q)], zv[TL::J(q)], acc[s],
+                                                          0, 0, 0);
+    }
+    if constexpr (WV < NT) {
+        fsum = __builtin_fmaf(tv, zv[WV], fsum);
+        ssum = ssum + zv[WV];
     }
 }
 
-// Accumulator tile -> M (row stride LD): the symmetric Gramian in full (an
-// off-diagonal tile is also stored transposed) and the two right-hand
-// columns KP, KP + 1.
+// Accumulator tiles -> M (row stride LD): the symmetric Gramian in full (an
+// off-diagonal tile is also stored transposed); the right-hand sums of
+// column block WV -> columns KP, KP + 1.
 template <int NT, int WV>
 __device__ __forceinline__ void als_dump(float* M, int LD, int lane,
-                                         const f32x16 (&acc)[AlsTiles<NT>::per_wave]) {
+                                         const f32x16 (&acc)[AlsTiles<NT>::per_wave],
+                                         float fsum, float ssum) {
     using TL = AlsTiles<NT>;
     constexpr int KP = NT * 32;
     const int col = lane & 31, h = lane >> 5;
@@ -103,13 +116,20 @@ __device__ __forceinline__ void als_dump(float* M, int LD, int lane,
         const int q = WV + 4 * s;
         if (q >= TL::count) continue;
         const int I = TL::I(q), J = TL::J(q);
-        if (J == NT && col >= 2) continue;
-        const int c = J < NT ? 32 * J + col : KP + col;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int row = 32 * I + (i & 3) + 8 * (i >> 2) + 4 * h;
-            M[row * LD + c] = acc[s][i];
-            if (I < J && J < NT) M[c * LD + row] = acc[s][i];
+            M[row * LD + 32 * J + col] = acc[s][i];
+            if (I < J) M[(32 * J + col) * LD + row] = acc[s][i];
+        }
+    }
+    if constexpr (WV < NT) {
+        // rows h = 0 and h = 1 of every K-step: lanes r and r + 32
+        fsum = fsum + __shfl_xor(fsum, 32, kWave);
+        ssum = ssum + __shfl_xor(ssum, 32, kWave);
+        if (h == 0) {
+            M[(32 * WV + col) * LD + KP] = fsum;
+            M[(32 * WV + col) * LD + KP + 1] = ssum;
         }
     }
 }
@@ -141,6 +161,7 @@ __device__ __forceinline__ void als_gram_wave(const AlsArgs& A, float* Zc, float
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[s][i] = 0.f;
     const int r = lane & 31, h = lane >> 5;
+    float fsum = 0.f, ssum = 0.f;
 
     auto load_ids = [&](int64_t c0, int (&ids)[NW], int& tid_id, float& rr) __attribute__((always_inline)) {
 #pragma unroll
@@ -201,12 +222,12 @@ __device__ __forceinline__ void als_gram_wave(const AlsArgs& A, float* Zc, float
         rr_cur = rr_next;
         const int steps = (m + 1) >> 1;
         for (int s = 0; s < steps; ++s) {
-            const int n = 2 * s + h;
-            als_kstep<NT, WV>(Zc + n * KP, tc[n], n < m ? 1.f : 0.f, r, acc);
+            const int n = 2 * s + h;                  // rows past m are zero rows
+            als_kstep<NT, WV>(Zc + n * KP, tc[n], r, acc, fsum, ssum);
         }
     }
     __syncthreads();                              // Zc is reused as M below
-    als_dump<NT, WV>(M, LD, lane, acc);
+    als_dump<NT, WV>(M, LD, lane, acc, fsum, ssum);
 }
 
 template <int NT>
@@ -222,6 +243,7 @@ __global__ __launch_bounds__(kAlsThreads) void k_als_solve(AlsArgs A) {
     const int e = blockIdx.x;
     const int64_t p0 = A.ptr[e], cnt = A.ptr[e + 1] - p0;
     if (cnt == 0) return;                         // no ratings: parameters kept
+    als_stamp(A, 0);
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     const int k = A.k;
@@ -239,6 +261,7 @@ __global__ __launch_bounds__(kAlsThreads) void k_als_solve(AlsArgs A) {
         if (lane == 0) red[0] = ts;
     }
     __syncthreads();
+    als_stamp(A, 1);
     const float g = red[0];
 
     // ---- symmetric elimination, register-tiled: thread (ty, tx) of a 16 x 16
@@ -249,7 +272,7 @@ __global__ __launch_bounds__(kAlsThreads) void k_als_solve(AlsArgs A) {
     constexpr int RX = KP / 16;                   // rows per thread
     constexpr int CY = KP / 16 + 1;               // columns per thread (+ f, s)
     constexpr int CW = 16 * CY;                   // published row width
-    __shared__ float rowbuf[2][CW];
+    __shared__ float rowbuf[2][CW + 1];           // row j | 1 / pivot
     const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
     float m[RX][CY];
 #pragma unroll
@@ -265,28 +288,36 @@ __global__ __launch_bounds__(kAlsThreads) void k_als_solve(AlsArgs A) {
             m[x][y] = v;
         }
     }
-    for (int j = 0; j < KP; ++j) {
-        float* rb = rowbuf[j & 1];
-        if (ty == (j & 15)) {
+    // pivot j = 16 jb + jj: the block index jb is a compile-time constant in
+    // each unrolled copy, so finished rows / columns (x, y < jb) are skipped
+    // statically and only the boundary tile (x or y == jb) is masked
 #pragma unroll
-            for (int x = 0; x < RX; ++x)
-                if (x == (j >> 4))
+    for (int jb = 0; jb < RX; ++jb) {
+#pragma clang loop unroll(disable)
+        for (int jj = 0; jj < 16; ++jj) {
+            float* rb = rowbuf[jj & 1];
+            if (ty == jj) {
 #pragma unroll
-                    for (int y = 0; y < CY; ++y) rb[tx + 16 * y] = m[x][y];
-        }
-        __syncthreads();
-        const float inv = 1.f / rb[j];
-        float rj[RX], cj[CY];
+                for (int y = jb; y < CY; ++y) rb[tx + 16 * y] = m[jb][y];
+                if (tx == jj) rb[CW] = 1.f / m[jb][jb];
+            }
+            __syncthreads();
+            const float inv = rb[CW];
+            float rj[RX], cj[CY];
 #pragma unroll
-        for (int x = 0; x < RX; ++x) rj[x] = rb[ty + 16 * x] * inv;
+            for (int x = jb; x < RX; ++x) rj[x] = rb[ty + 16 * x] * inv;
 #pragma unroll
-        for (int y = 0; y < CY; ++y) cj[y] = rb[tx + 16 * y];
+            for (int y = jb; y < CY; ++y) cj[y] = rb[tx + 16 * y];
 #pragma unroll
-        for (int x = 0; x < RX; ++x) {
-            const bool ra = ty + 16 * x > j;
+            for (int x = jb; x < RX; ++x) {
+                const bool ra = x > jb || ty > jj;
 #pragma unroll
-            for (int y = 0; y < CY; ++y)
-                if (ra && tx + 16 * y > j) m[x][y] = __builtin_fmaf(-rj[x], cj[y], m[x][y]);
+                for (int y = jb; y < CY; ++y) {
+                    const bool ok = ra && (y > jb || tx > jj);
+                    const float upd = __builtin_fmaf(-rj[x], cj[y], m[x][y]);
+                    m[x][y] = ok ? upd : m[x][y];
+                }
+            }
         }
     }
     // eliminated rows (D U | f' | s') back to M for the back substitution
@@ -298,6 +329,7 @@ __global__ __launch_bounds__(kAlsThreads) void k_als_solve(AlsArgs A) {
             if (b < KP + 2) M[(ty + 16 * x) * LD + b] = m[x][y];
         }
     __syncthreads();
+    als_stamp(A, 2);
 
     // ---- border (Schur complement) and back substitution: wave 0
     if (wv != 0) return;
@@ -332,6 +364,7 @@ __global__ __launch_bounds__(kAlsThreads) void k_als_solve(AlsArgs A) {
     if (v0 && a0 < k) out[a0] = x0;
     if (v1 && a1 < k) out[a1] = x1;
     if (lane == 0) A.bias[e] = b;
+    als_stamp(A, 3);
 }
 
 template <int NT>
@@ -353,11 +386,11 @@ using namespace mf;
 
 extern "C" int32_t mf_als_max_factors(void) { return kAlsMaxFactors; }
 
-extern "C" int mf_als_sweep(const int64_t* entity_ptr, const int32_t* other_ids,
+static int als_sweep(const int64_t* entity_ptr, const int32_t* other_ids,
                             const void* ratings, int32_t n_entities, double global_mean,
                             const void* other_biases, const void* other_features,
                             void* biases, void* features, int32_t n_factors, int32_t dtype,
-                            double reg, void* stream) {
+                            double reg, void* stream, int64_t* probe) {
     if (n_entities < 0 || n_factors < 1 || n_factors > kAlsMaxFactors) {
         set_error("mf_als_sweep: n_entities=%d / n_factors=%d (must be in [1, %d])", n_entities,
                   n_factors, kAlsMaxFactors);
@@ -377,9 +410,27 @@ extern "C" int mf_als_sweep(const int64_t* entity_ptr, const int32_t* other_ids,
     a.ob = static_cast<const float*>(other_biases);
     a.oq = static_cast<const float*>(other_features);
     a.bias = static_cast<float*>(biases); a.feat = static_cast<float*>(features);
-    a.k = n_factors; a.mu = (float)global_mean; a.reg = (float)reg;
+    a.k = n_factors; a.mu = (float)global_mean; a.reg = (float)reg; a.probe = probe;
     hipStream_t s = (hipStream_t)stream;
     if (n_factors <= 32) return als_go<1>(a, n_entities, s);
     if (n_factors <= 64) return als_go<2>(a, n_entities, s);
     return als_go<4>(a, n_entities, s);           // 96 columns do not tile 256 lanes
+}
+
+extern "C" int mf_als_sweep(const int64_t* entity_ptr, const int32_t* other_ids,
+                            const void* ratings, int32_t n_entities, double global_mean,
+                            const void* other_biases, const void* other_features,
+                            void* biases, void* features, int32_t n_factors, int32_t dtype,
+                            double reg, void* stream) {
+    return als_sweep(entity_ptr, other_ids, ratings, n_entities, global_mean, other_biases,
+                     other_features, biases, features, n_factors, dtype, reg, stream, nullptr);
+}
+
+extern "C" int mf_als_sweep_probe(const int64_t* entity_ptr, const int32_t* other_ids,
+                                  const void* ratings, int32_t n_entities, double global_mean,
+                                  const void* other_biases, const void* other_features,
+                                  void* biases, void* features, int32_t n_factors,
+                                  int32_t dtype, double reg, void* stream, int64_t* probe) {
+    return als_sweep(entity_ptr, other_ids, ratings, n_entities, global_mean, other_biases,
+                     other_features, biases, features, n_factors, dtype, reg, stream, probe);
 }

@@ -78,6 +78,8 @@ SIGNATURES = {
     "mf_als_sweep": (ctypes.c_int, [
         _P, _P, _P, _I32, _F64, _P, _P, _P, _P, _I32, _I32, _F64, _P]),
     "mf_als_max_factors": (ctypes.c_int32, []),
+    "mf_als_sweep_probe": (ctypes.c_int, [
+        _P, _P, _P, _I32, _F64, _P, _P, _P, _P, _I32, _I32, _F64, _P, _P]),
     "mf_replica_delta": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P]),
     "mf_sched_levels": (ctypes.c_int, [
         _P, _P, _I64, _P, _I32, _I32, _I32, _I32, _P, _P, _I64, _P]),
