@@ -326,11 +326,10 @@ def main() -> int:
     def rot_for(ep):          # colour-rotation seed of a strata epoch
         return (seed * 7919 + ep * 104729) & 0x7FFFFFFF
 
-    def run(ep, seq):
+    def run(ep, seq, timing=False):
         if strata:
-            eng.epoch_strata(seq, rot_for(ep), args.lr, args.reg)
-        else:
-            eng.epoch_colored(seq, args.lr, args.reg)
+            return eng.epoch_strata(seq, rot_for(ep), args.lr, args.reg, timing=timing)
+        return eng.epoch_colored(seq, args.lr, args.reg, timing=timing)
 
     def serial(ep, seq):
         if strata:
@@ -393,6 +392,7 @@ def main() -> int:
     reset_params()
     phase = not args.no_phase_timing
     launches_per_epoch = nb if strata else int(np.sum(np.diff(eng.colored) > 0))
+    persistent = False
     events = []     # (sgd start, sgd end, sse end) per timed epoch
 
     def epoch(ep, timed):
@@ -416,7 +416,19 @@ def main() -> int:
             events.append(ev)
 
     for ep in range(args.warmup):
-        epoch(ep, False)
+        if ep == 0 and strata:
+            # one synchronised epoch tells whether the persistent kernel ran
+            # (one launch) or the per-stratum fallback (B launches)
+            if exch is not None:
+                exch.begin_epoch()
+            _, n_launch = run(ep, seq_for(ep), timing=True)
+            if exch is not None:
+                exch.end_epoch()
+            eng.sse_async(ep)
+            persistent = n_launch == 1
+            launches_per_epoch = n_launch
+        else:
+            epoch(ep, False)
         log(f"warmup epoch {ep + 1}/{args.warmup}")
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -449,8 +461,14 @@ def main() -> int:
         # user-bias slice in and out (mf_strata.hpp) -- DESIGN.md section 4.
         survey_per_update = (16 * k + 28) if ts == 4 else (32 * k + 44)
         if strata:
-            alg_epoch = (n_local * (2 * k * ts + 8 + ts)
-                         + nb * 2 * (ni * (k + 1) * ts + n_users_local * ts))
+            # triples of every plan position (idle slots included), user row
+            # read + write per update, the user-bias slice in + out per block,
+            # the item slab (+ biases) in + out once per epoch (persistent) or
+            # once per stratum (per-stratum launches)
+            slab_passes = 1 if persistent else nb
+            alg_epoch = (plan.n_positions * (8 + ts) + n_local * 2 * k * ts
+                         + nb * 2 * n_users_local * ts
+                         + slab_passes * 2 * ni * (k + 1) * ts)
         else:
             alg_epoch = n_local * survey_per_update
         bytes_per_update = alg_epoch / n_local
@@ -462,14 +480,16 @@ def main() -> int:
             launches = launches_per_epoch * len(events)
             alg = alg_epoch * len(events)                           # algorithmic bytes
             achieved = alg / sgd_s / 1e9
-            traffic = traffic_from_profiles(args.workload, world, args.schedule)
+            traffic = traffic_from_profiles(args.workload, world, args.schedule
+                                            + ("_persistent" if persistent else ""))
             roofline = {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": "k_sgd_strata" if strata else "k_sgd_batch", "launches": launches,
+                "kernel": ("k_sgd_strata_epoch" if persistent else "k_sgd_strata") if strata
+                          else "k_sgd_batch", "launches": launches,
                 "avg_launch_us": sgd_s / launches * 1e6,
-                "avg_launch_note": "SGD phase time / launches (includes ~1.3 us "
-                                   "inter-kernel gaps)",
+                "avg_launch_note": "SGD phase time / launches (hipEvents around each "
+                                   "epoch's SGD launches on the launch stream)",
                 "alg_bytes_per_launch": alg / launches,
                 "bytes_per_update": bytes_per_update,
                 "survey_bytes_per_update": survey_per_update,

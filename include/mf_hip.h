@@ -54,8 +54,12 @@ enum {
     MF_FLAG_XCD_SWIZZLE = 1,  /* map consecutive tiles of a batch onto one XCD */
     MF_FLAG_NT_USER = 2,      /* stream user rows/biases/triples non-temporally */
     MF_FLAG_NT_ITEM = 4,      /* (unused by the current kernels)                */
-    MF_FLAG_XCD_CLAIM = 8     /* workgroups claim the tiles of the item slice of
+    MF_FLAG_XCD_CLAIM = 8,    /* workgroups claim the tiles of the item slice of
                                  the XCD they run on (needs `workspace`)        */
+    MF_FLAG_PERSISTENT = 16   /* mf_sgd_epoch_strata: the whole epoch in one
+                                 launch, item slabs resident in LDS (needs
+                                 `workspace`; falls back to one launch per
+                                 stratum when the grid cannot be co-resident) */
 };
 
 const char* mf_last_error(void);
@@ -133,8 +137,16 @@ size_t mf_sgd_workspace_bytes(int32_t n_launch);
  * slice of its user range in LDS and applies the block's steps starting at
  * step (mix(seed, block) mod n_steps), one LDS barrier apart.
  * max_block_items / max_block_users size the LDS (mf_strata_lds_bytes must
- * not exceed mf_strata_lds_limit()).  kernel_ms (HOST, optional): elapsed ms
- * of the whole call and the launch count (synchronises).
+ * not exceed mf_strata_lds_limit()).  flags: MF_FLAG_PERSISTENT runs the
+ * strata of strata_seq in ONE launch: workgroup w keeps item slab w in LDS
+ * throughout and, before each stratum, waits for the workgroup that last
+ * applied the same user range (bounded wait; on timeout it sets an error
+ * flag that mf_strata_status reports); it needs workspace (DEVICE, >=
+ * mf_strata_workspace_bytes(n_blocks, n_seq) bytes, zero-initialised once by
+ * the caller) and is used only when all n_blocks workgroups fit on the device
+ * at once, else the call falls back to one launch per stratum.  The result
+ * is the same sequential order either way.  kernel_ms (HOST, optional):
+ * elapsed ms of the whole call and the launch count (synchronises).
  */
 int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_ids,
                         const void* ratings, int64_t n_positions, int32_t n_blocks,
@@ -147,8 +159,12 @@ int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_ids,
                         int32_t n_items, int32_t n_factors, int32_t kernel, int32_t dtype,
                         double gamma, double lr, double reg, double min_rating,
                         double max_rating, int32_t update_user_params,
-                        int32_t update_item_params, int32_t flags, void* stream,
-                        double* kernel_ms);
+                        int32_t update_item_params, int32_t flags, void* workspace,
+                        size_t workspace_bytes, void* stream, double* kernel_ms);
+size_t mf_strata_workspace_bytes(int32_t n_blocks, int32_t n_seq);
+/* Synchronises `stream` and reports whether a persistent strata sweep using
+ * `workspace` gave up waiting (MF_ERR_HIP) since the workspace was zeroed. */
+int mf_strata_status(const void* workspace, int32_t n_blocks, void* stream);
 size_t mf_strata_lds_bytes(int32_t max_block_items, int32_t max_block_users,
                            int32_t n_factors, int32_t dtype);
 int32_t mf_strata_lds_limit(void);

@@ -252,6 +252,27 @@ extern "C" size_t mf_strata_lds_bytes(int32_t max_block_items, int32_t max_block
 
 extern "C" int32_t mf_strata_lds_limit(void) { return kLdsLimit; }
 
+extern "C" size_t mf_strata_workspace_bytes(int32_t n_blocks, int32_t n_seq) {
+    return n_blocks > 0 && n_seq >= 0 ? strata_ws_bytes(n_blocks, n_seq) : 0;
+}
+
+extern "C" int mf_strata_status(const void* workspace, int32_t n_blocks, void* stream) {
+    if (!workspace || n_blocks < 1) {
+        set_error("mf_strata_status: NULL workspace");
+        return MF_ERR_INVALID;
+    }
+    int32_t err = 0;
+    MF_HIP_CHECK(hipMemcpyAsync(&err, static_cast<const int32_t*>(workspace) + n_blocks,
+                                sizeof(int32_t), hipMemcpyDeviceToHost, (hipStream_t)stream));
+    MF_HIP_CHECK(hipStreamSynchronize((hipStream_t)stream));
+    if (err != 0) {
+        set_error("persistent strata sweep: a workgroup gave up waiting for its neighbour "
+                  "(workgroups not co-resident?); the parameters are invalid");
+        return MF_ERR_HIP;
+    }
+    return MF_OK;
+}
+
 extern "C" int32_t mf_strata_slots(int32_t n_factors, int32_t dtype) {
     if (n_factors < 0 || n_factors > kMaxFactors || (dtype != MF_F32 && dtype != MF_F64)) {
         set_error("mf_strata_slots: n_factors=%d / dtype=%d invalid", n_factors, dtype);
@@ -277,7 +298,8 @@ extern "C" int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_
                                    int32_t dtype, double gamma, double lr, double reg,
                                    double min_rating, double max_rating,
                                    int32_t update_user_params, int32_t update_item_params,
-                                   int32_t flags, void* stream, double* kernel_ms) {
+                                   int32_t flags, void* workspace, size_t workspace_bytes,
+                                   void* stream, double* kernel_ms) {
     if (n_positions < 0 || n_blocks < 0 || n_seq < 0 || n_users < 0 || n_items < 0 ||
         max_block_items < 0 || max_block_users < 0 || n_slots < 1) {
         set_error("negative size");
@@ -304,13 +326,13 @@ extern "C" int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_
         set_error("NULL parameter array");
         return MF_ERR_INVALID;
     }
-    (void)flags;
     StrataParams P{user_ids, item_ids, ratings, user_bounds, item_bounds, block_steps,
                    n_blocks, n_slots, max_block_items, max_block_users,
                    strata_seq, n_seq, seed, global_mean, user_biases, item_biases,
                    user_features, item_features, n_factors, kernel, gamma, lr, reg,
                    min_rating, max_rating, update_user_params ? 1 : 0,
-                   update_item_params ? 1 : 0, flags, (hipStream_t)stream, kernel_ms};
+                   update_item_params ? 1 : 0, flags, workspace, workspace_bytes, n_users,
+                   (hipStream_t)stream, kernel_ms};
     if (dtype == MF_F32) return strata_launch_f32(P);
     if (dtype == MF_F64) return strata_launch_f64(P);
     set_error("unknown dtype code %d", dtype);

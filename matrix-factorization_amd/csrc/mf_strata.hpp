@@ -69,6 +69,7 @@ struct StrataArgs {
     int32_t k;
     int32_t upd_user;
     int32_t upd_item;
+    uint64_t p_bytes;        // bytes of P (write-through buffer stores: < 4 GiB)
     Hyper<T> h;
 };
 
@@ -96,46 +97,22 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-template <typename T, int W, int GS, int V, int KERN, int S>
-__global__ __launch_bounds__(kStrataThreads) void k_sgd_strata(StrataArgs<T> A) {
+// The steps of block `blk` (user range from ulo, item range from ilo): the
+// software-pipelined sweep described at the top of this file.  Qs / Bis / Bus
+// are the LDS images of the item slab, its biases and the user-bias slice.
+// WT: user rows are stored write-through (sc1 buffer stores), the hand-off
+// form of the persistent kernel (no L2 write-back fence needed).
+template <typename T, int W, int GS, int V, int KERN, int S, bool WT = false>
+__device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk, int ulo, int ilo,
+                                             T* Qs, T* Bis, T* Bus, const Hyper<T> h) {
     using VT = typename VecOf<T, W>::type;
     constexpr int R = kWave / GS;
     constexpr int RPW = S * R;
     constexpr int NS = kStrataWaves * RPW;
-    static_assert(RPW <= kWave, "one lane per rating slot for the triple loads");
-    extern __shared__ __align__(16) unsigned char smem[];
-
-    const int B = A.B;
-    const int w = blockIdx.x;
-    const int ub = (w + A.s) % B;
-    const int64_t blk = (int64_t)A.s * B + w;
-    const int ilo = A.ibnd[w], nqi = A.ibnd[w + 1] - ilo;
-    const int ulo = A.ubnd[ub], nus = A.ubnd[ub + 1] - ulo;
     const int k = A.k;
     const int kv = k / W;
-    // field by field: an aggregate copy of the kernel-argument struct ends up
-    // in scratch once the step lambda captures it
-    Hyper<T> h;
-    h.mu = A.h.mu; h.lr = A.h.lr; h.reg = A.h.reg; h.gamma = A.h.gamma;
-    h.a = A.h.a; h.c = A.h.c; h.lo = A.h.lo; h.hi = A.h.hi;
-    T* Qs = reinterpret_cast<T*>(smem);
-    T* Bis = Qs + (size_t)nqi * k;
-    T* Bus = Bis + nqi;
-
-    // ---- stage the item slab and the bias slices (contiguous, coalesced)
-    {
-        const VT* src = reinterpret_cast<const VT*>(A.Q + (int64_t)ilo * k);
-        VT* dst = reinterpret_cast<VT*>(Qs);
-        const int nv = nqi * kv;
-#pragma unroll 4
-        for (int t = threadIdx.x; t < nv; t += kStrataThreads) dst[t] = src[t];
-        if constexpr (KERN != MF_RBF) {
-            for (int t = threadIdx.x; t < nqi; t += kStrataThreads) Bis[t] = A.Bi[ilo + t];
-            for (int t = threadIdx.x; t < nus; t += kStrataThreads) Bus[t] = A.Bu[ulo + t];
-        }
-    }
-    __syncthreads();
-
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t prs;
+    if constexpr (WT) prs = buf_rsrc(A.P, A.p_bytes);
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
     const int g = lane / GS;
@@ -237,7 +214,13 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata(StrataArgs<T> A) 
                 sgd_rows<T, KERN>(p[x][v], q[x][v], e, d, h, np, nq);
                 pprev[x][v] = np;
                 if (!(rwX.have[x] && vi < kv)) continue;
-                if (A.upd_user) st<true>(pw + vi, np);
+                if (A.upd_user) {
+                    if constexpr (WT)
+                        buf_st<16>(prs, (uint32_t)(((uint32_t)rwX.u[x] * (uint32_t)k +
+                                                    (uint32_t)(vi * W)) * sizeof(T)), np);
+                    else
+                        st<true>(pw + vi, np);
+                }
                 if (A.upd_item) qw[vi] = nq;
             }
             uprev[x] = (rwX.have[x] && A.upd_user) ? rwX.u[x] : -1;
@@ -256,22 +239,157 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata(StrataArgs<T> A) 
         step(t, ta, tb, ra, rb);
         if (t + 1 < nst) step(t + 1, tb, ta, rb, ra);
     }
-    __syncthreads();
+}
 
-    // ---- write the slab and the bias slices back
-    if (A.upd_item) {
-        VT* dst = reinterpret_cast<VT*>(A.Q + (int64_t)ilo * k);
-        const VT* src = reinterpret_cast<const VT*>(Qs);
-        const int nv = nqi * kv;
+// Stage the item slab (+ biases) of item range [ilo, ilo + nqi).
+template <typename T, int W, int KERN>
+__device__ __forceinline__ void strata_stage_slab(const StrataArgs<T>& A, int ilo, int nqi, T* Qs,
+                                                  T* Bis) {
+    using VT = typename VecOf<T, W>::type;
+    const int k = A.k;
+    const VT* src = reinterpret_cast<const VT*>(A.Q + (int64_t)ilo * k);
+    VT* dst = reinterpret_cast<VT*>(Qs);
+    const int nv = nqi * (k / W);
 #pragma unroll 4
-        for (int t = threadIdx.x; t < nv; t += kStrataThreads) dst[t] = src[t];
-        if constexpr (KERN != MF_RBF)
-            for (int t = threadIdx.x; t < nqi; t += kStrataThreads) A.Bi[ilo + t] = Bis[t];
-    }
+    for (int t = threadIdx.x; t < nv; t += kStrataThreads) dst[t] = src[t];
+    if constexpr (KERN != MF_RBF)
+        for (int t = threadIdx.x; t < nqi; t += kStrataThreads) Bis[t] = A.Bi[ilo + t];
+}
+
+// Write the item slab (+ biases) back.
+template <typename T, int W, int KERN>
+__device__ __forceinline__ void strata_store_slab(const StrataArgs<T>& A, int ilo, int nqi,
+                                                  const T* Qs, const T* Bis) {
+    using VT = typename VecOf<T, W>::type;
+    if (!A.upd_item) return;
+    const int k = A.k;
+    VT* dst = reinterpret_cast<VT*>(A.Q + (int64_t)ilo * k);
+    const VT* src = reinterpret_cast<const VT*>(Qs);
+    const int nv = nqi * (k / W);
+#pragma unroll 4
+    for (int t = threadIdx.x; t < nv; t += kStrataThreads) dst[t] = src[t];
+    if constexpr (KERN != MF_RBF)
+        for (int t = threadIdx.x; t < nqi; t += kStrataThreads) A.Bi[ilo + t] = Bis[t];
+}
+
+__device__ __forceinline__ Hyper<float> hyper_regs(const Hyper<float>& s) {
+    // field by field: an aggregate copy of the kernel-argument struct ends up
+    // in scratch once the step lambdas capture it
+    Hyper<float> h;
+    h.mu = s.mu; h.lr = s.lr; h.reg = s.reg; h.gamma = s.gamma;
+    h.a = s.a; h.c = s.c; h.lo = s.lo; h.hi = s.hi;
+    return h;
+}
+__device__ __forceinline__ Hyper<double> hyper_regs(const Hyper<double>& s) {
+    Hyper<double> h;
+    h.mu = s.mu; h.lr = s.lr; h.reg = s.reg; h.gamma = s.gamma;
+    h.a = s.a; h.c = s.c; h.lo = s.lo; h.hi = s.hi;
+    return h;
+}
+
+// One stratum per launch: workgroup w applies block (A.s, w).
+template <typename T, int W, int GS, int V, int KERN, int S>
+__global__ __launch_bounds__(kStrataThreads) void k_sgd_strata(StrataArgs<T> A) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int B = A.B;
+    const int w = blockIdx.x;
+    const int ub = (w + A.s) % B;
+    const int64_t blk = (int64_t)A.s * B + w;
+    const int ilo = A.ibnd[w], nqi = A.ibnd[w + 1] - ilo;
+    const int ulo = A.ubnd[ub], nus = A.ubnd[ub + 1] - ulo;
+    T* Qs = reinterpret_cast<T*>(smem);
+    T* Bis = Qs + (size_t)nqi * A.k;
+    T* Bus = Bis + nqi;
+    strata_stage_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
+    if constexpr (KERN != MF_RBF)
+        for (int t = threadIdx.x; t < nus; t += kStrataThreads) Bus[t] = A.Bu[ulo + t];
+    __syncthreads();
+    strata_block<T, W, GS, V, KERN, S>(A, blk, ulo, ilo, Qs, Bis, Bus, hyper_regs(A.h));
+    __syncthreads();
+    strata_store_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
     if constexpr (KERN != MF_RBF) {
         if (A.upd_user)
             for (int t = threadIdx.x; t < nus; t += kStrataThreads) A.Bu[ulo + t] = Bus[t];
     }
+}
+
+// Bounded wait of the persistent kernel (~1 s of polling, then give up: the
+// error flag is set and the workgroup leaves, so the grid always drains).
+constexpr int64_t kStrataSpinLimit = (int64_t)1 << 24;
+
+// The whole epoch in one launch (MF_FLAG_PERSISTENT): workgroup w keeps item
+// slab w in LDS for every stratum and walks the strata of `seq`; before
+// position t it waits until the workgroup that applied position t - 1 to the
+// same user range, w' = (w + seq[t] - seq[t-1]) mod B, has published
+// done[w'] >= t.  Hand-off (cdna_hip_programming.md Guideline 16, R1): the
+// block's user rows and user-bias slice are stored write-through (sc1), every
+// storing wave drains (vmcnt(0)), a barrier, one relaxed agent-scope flag
+// store; the consumer polls relaxed, one agent acquire (this CU's L1
+// invalidated), drain, barrier, plain loads.  The user rows cross XCDs
+// through memory; the item slab never leaves the CU.  The result is the same sequential order as one
+// launch per stratum.  All B workgroups must be co-resident (the launcher
+// checks occupancy before choosing this kernel).
+template <typename T, int W, int GS, int V, int KERN, int S>
+__global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<T> A,
+                                                                    const int32_t* seq,
+                                                                    int32_t n_seq, int32_t* done,
+                                                                    int32_t* err) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int s_abort;
+    const int B = A.B;
+    const int w = blockIdx.x;
+    const int ilo = A.ibnd[w], nqi = A.ibnd[w + 1] - ilo;
+    T* Qs = reinterpret_cast<T*>(smem);
+    T* Bis = Qs + (size_t)nqi * A.k;
+    T* Bus = Bis + nqi;
+    const Hyper<T> h = hyper_regs(A.h);
+    strata_stage_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
+    for (int t = 0; t < n_seq; ++t) {
+        const int s = seq[t];
+        const int ub = (w + s) % B;
+        const int ulo = A.ubnd[ub], nus = A.ubnd[ub + 1] - ulo;
+        if (threadIdx.x == 0) {
+            int ab = 0;
+            if (t > 0) {
+                const int wd = (w + s - seq[t - 1] + 2 * B) % B;
+                int64_t spins = 0;
+                while (__hip_atomic_load(done + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < t) {
+                    __builtin_amdgcn_s_sleep(2);
+                    if (++spins > kStrataSpinLimit ||
+                        __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ab = 1;
+                        break;
+                    }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");     // drop stale L1 lines
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // ... before the barrier
+            }
+            s_abort = ab;
+        }
+        __syncthreads();
+        if (s_abort) return;
+        if constexpr (KERN != MF_RBF)
+            for (int x = threadIdx.x; x < nus; x += kStrataThreads) Bus[x] = A.Bu[ulo + x];
+        __syncthreads();
+        strata_block<T, W, GS, V, KERN, S, true>(A, (int64_t)s * B + w, ulo, ilo, Qs, Bis, Bus,
+                                                 h);
+        __syncthreads();
+        if constexpr (KERN != MF_RBF) {
+            if (A.upd_user)
+                for (int x = threadIdx.x; x < nus; x += kStrataThreads)
+                    __hip_atomic_store(A.Bu + ulo + x, Bus[x], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);     // write-through
+        }
+        // every storing wave drains its write-through stores, then one lane
+        // signals (no L2 write-back fence: nothing handed off sits dirty in L2)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0)
+            __hip_atomic_store(done + w, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    strata_store_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
 }
 
 struct StrataParams {
@@ -281,8 +399,27 @@ struct StrataParams {
     const int32_t* seq; int32_t n_seq; uint32_t seed;
     double mu; void* bu; void* bi; void* P; void* Q; int32_t k; int32_t kernel;
     double gamma, lr, reg, lo, hi; int32_t uu, ui, flags;
+    void* ws; size_t ws_bytes; int64_t n_users;
     hipStream_t stream; double* kernel_ms;
 };
+
+// workspace of the persistent kernel: done[B], err, seq[n_seq] (int32)
+inline size_t strata_ws_bytes(int32_t B, int32_t n_seq) {
+    return sizeof(int32_t) * ((size_t)B + 1 + (size_t)n_seq);
+}
+
+// Can all B workgroups of `kfn` be resident at once (the persistent kernel's
+// waits need it)?
+inline bool strata_coresident(const void* kfn, int B, size_t lds) {
+    int dev = 0, cus = 0, per_cu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return false;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kStrataThreads, lds) !=
+        hipSuccess)
+        return false;
+    return (int64_t)cus * per_cu >= B;
+}
 
 // NS of the row layout (W, GS, V) that dispatch_rows picks for (k, dtype)
 template <typename T>
@@ -325,6 +462,7 @@ struct StrataRun {
         a.Bu = static_cast<T*>(p.bu); a.Bi = static_cast<T*>(p.bi);
         a.ubnd = p.ubnd; a.ibnd = p.ibnd; a.bstep = p.bstep;
         a.B = p.B; a.seed = p.seed; a.k = p.k; a.upd_user = p.uu; a.upd_item = p.ui;
+        a.p_bytes = (uint64_t)p.n_users * (uint64_t)p.k * sizeof(T);
         a.h = make_hyper<T>(p.mu, p.lr, p.reg, p.gamma, p.lo, p.hi);
         hipEvent_t ev[2] = {nullptr, nullptr};
         if (p.kernel_ms) {
@@ -332,9 +470,30 @@ struct StrataRun {
             MF_HIP_CHECK(hipEventCreate(&ev[1]));
             MF_HIP_CHECK(hipEventRecord(ev[0], p.stream));
         }
-        for (int32_t t = 0; t < p.n_seq; ++t) {
-            a.s = p.seq[t];
-            hipLaunchKernelGGL(kfn, dim3((unsigned)p.B), dim3(kStrataThreads), lds, p.stream, a);
+        bool persistent = false;
+        if ((p.flags & MF_FLAG_PERSISTENT) && p.ws &&
+            p.ws_bytes >= strata_ws_bytes(p.B, p.n_seq) && a.p_bytes < 0xFFFFFFFFull) {
+            auto efn = k_sgd_strata_epoch<T, W, GS, V, KERN, S>;
+            MF_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(efn),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            persistent = strata_coresident(reinterpret_cast<const void*>(efn), p.B, lds);
+            if (persistent) {
+                int32_t* done = static_cast<int32_t*>(p.ws);
+                int32_t* err = done + p.B;
+                int32_t* dseq = err + 1;
+                MF_HIP_CHECK(hipMemsetAsync(done, 0, sizeof(int32_t) * (size_t)p.B, p.stream));
+                MF_HIP_CHECK(hipMemcpyAsync(dseq, p.seq, sizeof(int32_t) * (size_t)p.n_seq,
+                                            hipMemcpyHostToDevice, p.stream));
+                hipLaunchKernelGGL(efn, dim3((unsigned)p.B), dim3(kStrataThreads), lds, p.stream,
+                                   a, (const int32_t*)dseq, p.n_seq, done, err);
+            }
+        }
+        if (!persistent) {
+            for (int32_t t = 0; t < p.n_seq; ++t) {
+                a.s = p.seq[t];
+                hipLaunchKernelGGL(kfn, dim3((unsigned)p.B), dim3(kStrataThreads), lds, p.stream,
+                                   a);
+            }
         }
         hipError_t le = hipGetLastError();
         int rc = le == hipSuccess ? MF_OK : hip_fail(le, "k_sgd_strata launch");
@@ -346,7 +505,7 @@ struct StrataRun {
                 if (e == hipSuccess) e = hipEventElapsedTime(&ms, ev[0], ev[1]);
                 if (e != hipSuccess) rc = hip_fail(e, "strata timing");
                 p.kernel_ms[0] = ms;
-                p.kernel_ms[1] = (double)p.n_seq;
+                p.kernel_ms[1] = persistent ? 1.0 : (double)p.n_seq;
             }
             (void)hipEventDestroy(ev[0]);
             (void)hipEventDestroy(ev[1]);

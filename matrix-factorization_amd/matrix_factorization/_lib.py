@@ -20,6 +20,7 @@ MF_FLAG_XCD_SWIZZLE = 1
 MF_FLAG_NT_USER = 2
 MF_FLAG_NT_ITEM = 4
 MF_FLAG_XCD_CLAIM = 8
+MF_FLAG_PERSISTENT = 16
 MF_ERR_CAPACITY = 3
 MF_DELTA_TAKE, MF_DELTA_APPLY = 0, 1
 KERNEL_CODES = {"linear": MF_LINEAR, "sigmoid": MF_SIGMOID, "rbf": MF_RBF}
@@ -51,7 +52,9 @@ SIGNATURES = {
         _I32, _I32, _I32,                             # n_users, n_items, k
         _I32, _I32, _F64, _F64, _F64, _F64, _F64,     # kernel dtype gamma lr reg min max
         _I32, _I32, _I32,                             # upd_u upd_i flags
-        _P, _PD]),                                    # stream kernel_ms
+        _P, ctypes.c_size_t, _P, _PD]),               # ws ws_bytes stream kernel_ms
+    "mf_strata_workspace_bytes": (ctypes.c_size_t, [_I32, _I32]),
+    "mf_strata_status": (ctypes.c_int, [_P, _I32, _P]),
     "mf_strata_lds_bytes": (ctypes.c_size_t, [_I32, _I32, _I32, _I32]),
     "mf_strata_lds_limit": (ctypes.c_int32, []),
     "mf_strata_slots": (ctypes.c_int32, [_I32, _I32]),

@@ -407,16 +407,28 @@ class SGDEngine:
         self.strata = plan
         return plan
 
+    # one launch per epoch with the item slabs resident (MF_FLAG_PERSISTENT);
+    # False: one launch per stratum
+    strata_persistent = True
+
     def epoch_strata(self, seq: Optional[np.ndarray], seed: int, lr: float, reg: float,
-                     update_user: bool = True, update_item: bool = True, timing=False):
+                     update_user: bool = True, update_item: bool = True, timing=False,
+                     persistent: Optional[bool] = None):
         """Apply the strata listed in ``seq`` (a permutation of range(B) is
-        one epoch) with colour rotation ``seed``."""
+        one epoch) with step rotation ``seed``."""
         pl = self.strata
         if pl is None:
             raise RuntimeError("call prepare_strata() first")
         seq = (np.arange(pl.B, dtype=np.int32) if seq is None
                else np.ascontiguousarray(seq, np.int32))
         ms = (ctypes.c_double * 2)() if timing else None
+        if persistent is None:
+            persistent = self.strata_persistent
+        flags = _lib.MF_FLAG_PERSISTENT if persistent else 0
+        wsb = int(_lib.load().mf_strata_workspace_bytes(pl.B, len(seq)))
+        if getattr(self, "_strata_ws", None) is None or self._strata_ws.numel() * 4 < wsb:
+            # zeroed once: the error flag is sticky until check_strata() raises
+            self._strata_ws = torch.zeros((wsb + 3) // 4, dtype=torch.int32, device=self.dev)
         with torch.cuda.device(self.dev):
             _lib.call("mf_sgd_epoch_strata", _tp(pl.d_u), _tp(pl.d_i), _tp(pl.d_r),
                       pl.n_positions, pl.B, _tp(pl.d_ubnd), _tp(pl.d_ibnd), _tp(pl.d_bstep),
@@ -425,8 +437,17 @@ class SGDEngine:
                       _tp(self.P), _tp(self.Q), self.n_users, self.n_items, self.k,
                       self.kcode, self.dcode, self.gamma, float(lr), float(reg),
                       self.min_rating, self.max_rating, int(update_user), int(update_item),
-                      0, self.stream, ms)
+                      flags, _tp(self._strata_ws), self._strata_ws.numel() * 4, self.stream, ms)
         return (ms[0], int(ms[1])) if timing else None
+
+    def check_strata(self) -> None:
+        """Synchronise and raise if a persistent strata sweep gave up waiting
+        (its parameters would be invalid)."""
+        ws = getattr(self, "_strata_ws", None)
+        if ws is None:
+            return
+        with torch.cuda.device(self.dev):
+            _lib.call("mf_strata_status", _tp(ws), self.strata.B, self.stream)
 
     def epoch_exact(self, order: np.ndarray, lr: float, reg: float,
                     update_user: bool = True, update_item: bool = True,
@@ -682,6 +703,8 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
             print("Epoch ", epoch + 1, "/", n_epochs, " -  train_rmse:", rmse)
         if on_epoch is not None:
             on_epoch(epoch)
+    if schedule == "strata":
+        engine.check_strata()
     if verbose != 1:
         train_rmse = engine.rmse_values(n_epochs)
     return train_rmse

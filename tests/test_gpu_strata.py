@@ -145,3 +145,26 @@ def test_kernelmf_strata_fit_converges():
     assert abs(ms.train_rmse[-1] - me.train_rmse[-1]) < 2e-3
     pred = ms.predict(X.iloc[:100])
     assert len(pred) == 100 and np.all(np.isfinite(pred))
+
+
+@pytest.mark.parametrize("dtype,B", [("float64", 6), ("float32", 16)])
+def test_persistent_epoch_equals_per_stratum_launches(dtype, B):
+    """MF_FLAG_PERSISTENT (one launch per epoch, item slabs resident, neighbour
+    waits) applies the same sequential order as one launch per stratum: the
+    parameters are bit-identical."""
+    nu, ni, nnz, k = 3000, 1200, 150000, 64
+    u, i, r = _synthetic(51, nu, ni, nnz)
+    rs = np.random.RandomState(52)
+    P = rs.normal(0, 0.1, (nu, k)); Q = rs.normal(0, 0.1, (ni, k))
+    bu = rs.normal(0, 0.1, nu); bi = rs.normal(0, 0.1, ni)
+    out = []
+    for persistent in (True, False):
+        eng = _engine(u, i, r, nu, ni, k, "linear", dtype, P, Q, bu, bi)
+        eng.prepare_strata(n_blocks=B)
+        for ep in range(3):
+            seq = np.random.RandomState(ep).permutation(B).astype(np.int32)
+            eng.epoch_strata(seq, 1000 + ep, lr=0.01, reg=0.02, persistent=persistent)
+        eng.check_strata()
+        out.append(eng.params_numpy())
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
