@@ -100,8 +100,9 @@ __device__ __forceinline__ void lds_barrier() {
 // The steps of block `blk` (user range from ulo, item range from ilo): the
 // software-pipelined sweep described at the top of this file.  Qs / Bis / Bus
 // are the LDS images of the item slab, its biases and the user-bias slice.
-// WT: user rows are stored write-through (sc1 buffer stores), the hand-off
-// form of the persistent kernel (no L2 write-back fence needed).
+// WT: user rows are loaded and stored with sc1 buffer ops (write-through
+// stores, L1-bypassing loads), the hand-off form of the persistent kernel: no
+// L2 write-back fence on the producer, no L1 invalidate on the consumer.
 template <typename T, int W, int GS, int V, int KERN, int S, bool WT = false>
 __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk, int ulo, int ilo,
                                              T* Qs, T* Bis, T* Bus, const Hyper<T> h) {
@@ -162,7 +163,13 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
 #pragma unroll
             for (int v = 0; v < V; ++v) {
                 const int vi = v * GS + l;
-                o.p[x][v] = ld<true>(row + (vi < kv ? vi : kv - 1));     // kv >= 1
+                const int vc = vi < kv ? vi : kv - 1;                    // kv >= 1
+                if constexpr (WT)   // sc1: L2-served, never a stale L1 line
+                    o.p[x][v] = buf_ld<16, VT>(
+                        prs, (uint32_t)(((uint32_t)o.u[x] * (uint32_t)k + (uint32_t)(vc * W)) *
+                                        sizeof(T)));
+                else
+                    o.p[x][v] = ld<true>(row + vc);
             }
         }
     };
@@ -324,9 +331,9 @@ constexpr int64_t kStrataSpinLimit = (int64_t)1 << 24;
 // done[w'] >= t.  Hand-off (cdna_hip_programming.md Guideline 16, R1): the
 // block's user rows and user-bias slice are stored write-through (sc1), every
 // storing wave drains (vmcnt(0)), a barrier, one relaxed agent-scope flag
-// store; the consumer polls relaxed, one agent acquire (this CU's L1
-// invalidated), drain, barrier, plain loads.  The user rows cross XCDs
-// through memory; the item slab never leaves the CU.  The result is the same sequential order as one
+// store; the consumer polls relaxed and reads every handed-off byte with sc1
+// loads (L2-served), so no fence is needed on either side.  The user rows
+// cross XCDs through memory; the item slab never leaves the CU.  The result is the same sequential order as one
 // launch per stratum.  All B workgroups must be co-resident (the launcher
 // checks occupancy before choosing this kernel).
 template <typename T, int W, int GS, int V, int KERN, int S>
@@ -362,15 +369,18 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<
                         break;
                     }
                 }
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");     // drop stale L1 lines
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");        // ... before the barrier
+                // every load of handed-off bytes below is sc1: no L1 invalidate,
+                // only keep the compiler from hoisting them above the poll
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             }
             s_abort = ab;
         }
         __syncthreads();
         if (s_abort) return;
         if constexpr (KERN != MF_RBF)
-            for (int x = threadIdx.x; x < nus; x += kStrataThreads) Bus[x] = A.Bu[ulo + x];
+            for (int x = threadIdx.x; x < nus; x += kStrataThreads)
+                Bus[x] = __hip_atomic_load(A.Bu + ulo + x, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);          // sc1 load
         __syncthreads();
         strata_block<T, W, GS, V, KERN, S, true>(A, (int64_t)s * B + w, ulo, ilo, Qs, Bis, Bus,
                                                  h);
