@@ -26,6 +26,7 @@
 //      wave 0: b_e = (sum t - s'.D^-1 f') / (n + reg - s'.D^-1 s'),
 //      w_e = U^-1 D^-1 (f' - b_e s')   (f' = U^-T f, s' = U^-T s).
 #include <algorithm>
+#include <utility>
 
 #include "mf_common.hpp"
 
@@ -231,7 +232,7 @@ __device__ __forceinline__ void als_gram_wave(const AlsArgs& A, float* Zc, float
 }
 
 template <int NT>
-__global__ __launch_bounds__(kAlsThreads) void k_als_solve(AlsArgs A) {
+__global__ __launch_bounds__(kAlsThreads, 2) void k_als_solve(AlsArgs A) {
     constexpr int KP = NT * 32;
     constexpr int LD = KP + 3;                    // odd stride: column reads conflict-free
     extern __shared__ __align__(16) float lds[];
@@ -272,7 +273,7 @@ __global__ __launch_bounds__(kAlsThreads) void k_als_solve(AlsArgs A) {
     constexpr int RX = KP / 16;                   // rows per thread
     constexpr int CY = KP / 16 + 1;               // columns per thread (+ f, s)
     constexpr int CW = 16 * CY;                   // published row width
-    __shared__ float rowbuf[2][CW + 1];           // row j | 1 / pivot
+    __shared__ float rowbuf[2][4][CW];            // four pivot rows, double-buffered
     const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
     float m[RX][CY];
 #pragma unroll
@@ -288,34 +289,75 @@ __global__ __launch_bounds__(kAlsThreads) void k_als_solve(AlsArgs A) {
             m[x][y] = v;
         }
     }
-    // pivot j = 16 jb + jj: the block index jb is a compile-time constant in
-    // each unrolled copy, so finished rows / columns (x, y < jb) are skipped
-    // statically and only the boundary tile (x or y == jb) is masked
+    // Pivots in groups of four, one barrier per group: the wave holding rows
+    // j0..j0+3 (ty = 4 jq .. 4 jq + 3) publishes them; every thread eliminates
+    // the 4 x 4 diagonal block redundantly on the entries it needs (its
+    // columns tx + 16y, its rows' columns ty + 16x, by symmetry) and applies
+    // the rank-4 update to its trailing elements.  The row-block index jb is
+    // a compile-time constant in each unrolled copy, so finished rows and
+    // columns (x, y < jb) are skipped statically.
 #pragma unroll
     for (int jb = 0; jb < RX; ++jb) {
 #pragma clang loop unroll(disable)
-        for (int jj = 0; jj < 16; ++jj) {
-            float* rb = rowbuf[jj & 1];
-            if (ty == jj) {
+        for (int jq = 0; jq < 4; ++jq) {
+            const int j0 = 16 * jb + 4 * jq;
+            float (*rb)[CW] = rowbuf[jq & 1];
+            const bool owner = (ty >> 2) == jq;
+            if (owner) {
 #pragma unroll
-                for (int y = jb; y < CY; ++y) rb[tx + 16 * y] = m[jb][y];
-                if (tx == jj) rb[CW] = 1.f / m[jb][jb];
+                for (int y = jb; y < CY; ++y) rb[ty & 3][tx + 16 * y] = m[jb][y];
             }
             __syncthreads();
-            const float inv = rb[CW];
-            float rj[RX], cj[CY];
+            float D[4][4], PR[4][CY], inv[4], f[4][4];
 #pragma unroll
-            for (int x = jb; x < RX; ++x) rj[x] = rb[ty + 16 * x] * inv;
+            for (int r = 0; r < 4; ++r) {
 #pragma unroll
-            for (int y = jb; y < CY; ++y) cj[y] = rb[tx + 16 * y];
+                for (int c = 0; c < 4; ++c) D[r][c] = rb[r][j0 + c];
+#pragma unroll
+                for (int y = jb; y < CY; ++y) PR[r][y] = rb[r][tx + 16 * y];
+            }
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                inv[r] = 1.f / D[r][r];
+#pragma unroll
+                for (int r2 = r + 1; r2 < 4; ++r2) {
+                    f[r][r2] = D[r][r2] * inv[r];
+#pragma unroll
+                    for (int c = r2; c < 4; ++c)
+                        D[r2][c] = __builtin_fmaf(-f[r][r2], D[r][c], D[r2][c]);
+#pragma unroll
+                    for (int y = jb; y < CY; ++y)
+                        PR[r2][y] = __builtin_fmaf(-f[r][r2], PR[r][y], PR[r2][y]);
+                }
+            }
+            // rank-4 update; element (a, b) takes pivot j0 + r when a and b
+            // both lie past it -- for the pivot rows' owners this yields the
+            // row eliminated by the earlier pivots of the group (final).  The
+            // multipliers of row a are the pivot rows at column a (symmetry),
+            // read here and eliminated like PR.
 #pragma unroll
             for (int x = jb; x < RX; ++x) {
-                const bool ra = x > jb || ty > jj;
+                const int a = ty + 16 * x;
+                float pc[4], l4[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) pc[r] = rb[r][a];
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+#pragma unroll
+                    for (int r2 = r + 1; r2 < 4; ++r2)
+                        pc[r2] = __builtin_fmaf(-f[r][r2], pc[r], pc[r2]);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) l4[r] = a > j0 + r ? pc[r] * inv[r] : 0.f;
 #pragma unroll
                 for (int y = jb; y < CY; ++y) {
-                    const bool ok = ra && (y > jb || tx > jj);
-                    const float upd = __builtin_fmaf(-rj[x], cj[y], m[x][y]);
-                    m[x][y] = ok ? upd : m[x][y];
+                    const int b = tx + 16 * y;
+                    float upd = m[x][y];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float lr = b > j0 + r ? l4[r] : 0.f;
+                        upd = __builtin_fmaf(-lr, PR[r][y], upd);
+                    }
+                    m[x][y] = upd;
                 }
             }
         }
