@@ -446,6 +446,8 @@ def main() -> int:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    if strata:
+        eng.check_strata()          # raises if a persistent sweep gave up waiting
     n_ep = args.warmup + args.steps
     rmse = global_rmse(eng, n_ep, nnz)
 
