@@ -403,6 +403,36 @@ int mf_strata_plan_fetch(const mf_strata_plan* plan, int32_t* sched_out,
                          int64_t* block_steps);
 void mf_strata_plan_free(mf_strata_plan* plan);
 
+/* ---------------------------------------------------------------------------
+ * fit() preprocessing, host only (mf_prep.cpp).  Replaces the three costly
+ * steps of RecommenderBase._preprocess_data (recommender_base.py:97-173 of
+ * the reference) for integer ids, with identical results:
+ *
+ * mf_legacy_shuffle      numpy.random.RandomState.shuffle(data) of a 1-D
+ *     8-byte array, drawn from the MT19937 state (key[624], *pos) given and
+ *     advancing it exactly as NumPy does (numpy 2.2 mtrand _shuffle_raw +
+ *     random_interval).  On arange(n) this is permutation(n), which is the
+ *     draw of X.sample(frac=1, replace=False) (recommender_base.py:131 =
+ *     RandomState.choice(n, n, replace=False)); on the row order it is the
+ *     per-epoch np.random.shuffle (kernel_matrix_factorization.py:371).
+ *     n <= 2^32 + 1 (NumPy's 32-bit draw branch); MF_ERR_INVALID otherwise.
+ * mf_pairs_duplicated    *has_dup = 1 iff two rows hold the same (a, b)
+ *     pair of integer ids (X.duplicated(subset=[user_id, item_id]).sum()
+ *     != 0, :127-128).
+ * mf_factorize           pd.factorize(vals, sort=False) of integer ids, as
+ *     X[col].unique() + the id map of the shuffled frame (:135-140):
+ *     uniques[0..*n_uniques) in first-appearance order (capacity n) and
+ *     codes[p] = position of vals[p] in uniques.
+ * mf_gather              dst[p] = src[idx[p]], idx[p] in [0, n_src), for
+ *     elem_bytes 4 or 8.
+ * Threads: min(16, cores) unless MF_HOST_THREADS is set. */
+int mf_legacy_shuffle(uint32_t* mt_key, int32_t* mt_pos, int64_t* data, int64_t n);
+int mf_pairs_duplicated(const int64_t* a, const int64_t* b, int64_t n, int32_t* has_dup);
+int mf_factorize(const int64_t* vals, int64_t n, int64_t* codes, int64_t* uniques,
+                 int64_t* n_uniques);
+int mf_gather(const void* src, int64_t n_src, int32_t elem_bytes, const int64_t* idx, int64_t n,
+              void* dst);
+
 #ifdef __cplusplus
 }
 #endif

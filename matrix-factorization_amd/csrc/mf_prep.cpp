@@ -1,0 +1,411 @@
+// mf_prep.cpp -- fit() preprocessing at 10^8 rows, host only.
+//
+// RecommenderBase._preprocess_data (recommender_base.py:120-141 of the
+// reference) spends a minute of fit() at C3 scale in pandas: the duplicate
+// pair check (:127), the row shuffle X.sample(frac=1) (:131) and the
+// first-appearance id maps (:135-138).  The GPU epochs of the same fit take
+// ~12 ms each.  These helpers give the same results faster:
+//
+//   mf_legacy_shuffle    NumPy's legacy RandomState.shuffle (numpy 2.2,
+//                        mtrand.pyx _shuffle_raw: for i = n-1 .. 1 swap
+//                        x[i], x[random_interval(i)]; distributions.c
+//                        random_interval: smallest all-ones mask >= max,
+//                        32-bit MT19937 draws & mask until <= max) with the
+//                        swap targets drawn a window ahead and prefetched;
+//                        the draws, and so the MT state afterwards, are
+//                        NumPy's.
+//   mf_pairs_duplicated  hash-partition of the rows by (user, item) pair
+//                        into cache-sized buckets, a hash set per bucket.
+//   mf_factorize         pd.factorize(sort=False): the same partition by
+//                        value keeps rows ascending inside a bucket, so a
+//                        per-bucket hash table sees each value's first row
+//                        first; code = number of first rows before it
+//                        (bitmap + prefix popcount).
+//   mf_gather            threaded, prefetched dst[p] = src[idx[p]].
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <thread>
+#include <vector>
+
+#include "../../include/mf_hip.h"
+
+namespace mf {
+void set_error(const char* fmt, ...);
+}
+using mf::set_error;
+
+namespace {
+
+int host_threads() {
+    if (const char* s = std::getenv("MF_HOST_THREADS")) {
+        const int v = std::atoi(s);
+        if (v > 0) return std::min(v, 256);
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(16u, hw));
+}
+
+// fn(t, lo, hi) over [0, n) cut into T contiguous chunks
+void parallel_chunks(int64_t n, int T, const std::function<void(int, int64_t, int64_t)>& fn) {
+    if (T <= 1 || n < (int64_t)1 << 16) {
+        fn(0, 0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(T);
+    for (int t = 0; t < T; ++t) {
+        const int64_t lo = n * t / T, hi = n * (t + 1) / T;
+        th.emplace_back(fn, t, lo, hi);
+    }
+    for (auto& x : th) x.join();
+}
+
+// ---------------------------------------------------------------- MT19937
+// The standard Mersenne Twister (Matsumoto & Nishimura 1998) as NumPy's
+// legacy bit generator keeps it: key[624] + position, tempered output.
+constexpr int kN = 624, kM = 397;
+constexpr uint32_t kMatrixA = 0x9908b0dfu, kUpper = 0x80000000u, kLower = 0x7fffffffu;
+
+struct MT {
+    uint32_t key[kN];
+    int pos;
+
+    void regen() {
+        int i = 0;
+        for (; i < kN - kM; ++i) {
+            const uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
+            key[i] = key[i + kM] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+        }
+        for (; i < kN - 1; ++i) {
+            const uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
+            key[i] = key[i + (kM - kN)] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+        }
+        const uint32_t y = (key[kN - 1] & kUpper) | (key[0] & kLower);
+        key[kN - 1] = key[kM - 1] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+        pos = 0;
+    }
+    uint32_t next() {
+        if (pos == kN) regen();
+        uint32_t y = key[pos++];
+        y ^= y >> 11;
+        y ^= (y << 7) & 0x9d2c5680u;
+        y ^= (y << 15) & 0xefc60000u;
+        y ^= y >> 18;
+        return y;
+    }
+    // random_interval(max) for max <= 0xffffffff
+    uint32_t interval(uint32_t max) {
+        if (max == 0) return 0;
+        uint32_t mask = max;
+        mask |= mask >> 1;
+        mask |= mask >> 2;
+        mask |= mask >> 4;
+        mask |= mask >> 8;
+        mask |= mask >> 16;
+        uint32_t v;
+        while ((v = next() & mask) > max) {
+        }
+        return v;
+    }
+};
+
+}  // namespace
+
+extern "C" int mf_legacy_shuffle(uint32_t* mt_key, int32_t* mt_pos, int64_t* data, int64_t n) {
+    if (!mt_key || !mt_pos || (n > 0 && !data) || n < 0) {
+        set_error("mf_legacy_shuffle: null pointer or negative n");
+        return MF_ERR_INVALID;
+    }
+    if (n - 1 > (int64_t)0xffffffffLL) {
+        set_error("mf_legacy_shuffle: n = %lld exceeds the 32-bit draw range", (long long)n);
+        return MF_ERR_INVALID;
+    }
+    if (*mt_pos < 0 || *mt_pos > kN) {
+        set_error("mf_legacy_shuffle: MT19937 position %d outside [0, %d]", *mt_pos, kN);
+        return MF_ERR_INVALID;
+    }
+    MT mt;
+    std::memcpy(mt.key, mt_key, sizeof(mt.key));
+    mt.pos = *mt_pos;
+    // Swap targets are drawn kWin positions ahead of the swap that uses them
+    // (the draws do not depend on the data) so the random line is in cache
+    // when the swap reaches it.
+    constexpr int kWin = 64;
+    uint32_t ring[kWin];
+    int64_t i = n - 1, drawn = n - 1;  // next swap index / next index to draw for
+    const int64_t pre = std::min<int64_t>(kWin, std::max<int64_t>(n - 1, 0));
+    for (int w = 0; w < pre; ++w, --drawn) {
+        const uint32_t j = mt.interval((uint32_t)drawn);
+        ring[drawn % kWin] = j;
+        __builtin_prefetch(data + j, 1, 1);
+    }
+    for (; i >= 1; --i) {
+        const int64_t j = ring[i % kWin];
+        if (drawn >= 1) {
+            const uint32_t jn = mt.interval((uint32_t)drawn);
+            ring[drawn % kWin] = jn;
+            __builtin_prefetch(data + jn, 1, 1);
+            --drawn;
+        }
+        const int64_t t = data[i];
+        data[i] = data[j];
+        data[j] = t;
+    }
+    std::memcpy(mt_key, mt.key, sizeof(mt.key));
+    *mt_pos = mt.pos;
+    return MF_OK;
+}
+
+namespace {
+
+int bucket_bits(int64_t n) {  // 2^R buckets of <= ~16K entries
+    int R = 1;
+    while (R < 16 && (n >> R) > (1 << 14)) ++R;
+    return R;
+}
+
+inline uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    return x ^ (x >> 31);
+}
+
+// Stable hash partition of rows [0, n) into 2^R buckets: bucket b owns the
+// destinations start[b] .. start[b+1], filled in ascending row order (chunk t
+// precedes chunk t+1 and each chunk is scattered in order) by emit(dst, row).
+template <class F, class E>
+void partition_rows(int64_t n, int R, int T, F bucket, std::vector<int64_t>& start, E emit) {
+    const int NB = 1 << R;
+    const int Tused = (T <= 1 || n < (int64_t)1 << 16) ? 1 : T;
+    std::vector<int64_t> count((size_t)Tused * NB, 0);
+    parallel_chunks(n, Tused, [&](int t, int64_t lo, int64_t hi) {
+        int64_t* c = count.data() + (size_t)t * NB;
+        for (int64_t p = lo; p < hi; ++p) ++c[bucket(p)];
+    });
+    start.assign((size_t)NB + 1, 0);
+    int64_t acc = 0;
+    for (int b = 0; b < NB; ++b) {
+        start[b] = acc;
+        for (int t = 0; t < Tused; ++t) {
+            int64_t& c = count[(size_t)t * NB + b];
+            const int64_t v = c;
+            c = acc;  // write cursor of chunk t in bucket b
+            acc += v;
+        }
+    }
+    start[NB] = acc;
+    parallel_chunks(n, Tused, [&](int t, int64_t lo, int64_t hi) {
+        int64_t* cur = count.data() + (size_t)t * NB;
+        for (int64_t p = lo; p < hi; ++p) emit(cur[bucket(p)]++, p);
+    });
+}
+
+// fn(b) for every bucket b, dynamically balanced over T threads; stops early
+// once `stop` is set
+template <class F>
+void for_buckets(int NB, int T, F fn, const std::atomic<int>* stop = nullptr) {
+    std::atomic<int> next{0};
+    auto work = [&]() {
+        for (int b; !(stop && stop->load(std::memory_order_relaxed)) &&
+                    (b = next.fetch_add(1)) < NB;)
+            fn(b);
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < std::min(T, NB); ++t) th.emplace_back(work);
+    work();
+    for (auto& x : th) x.join();
+}
+
+}  // namespace
+
+extern "C" int mf_pairs_duplicated(const int64_t* a, const int64_t* b, int64_t n,
+                                   int32_t* has_dup) {
+    if (!has_dup || n < 0 || (n > 0 && (!a || !b))) {
+        set_error("mf_pairs_duplicated: bad arguments");
+        return MF_ERR_INVALID;
+    }
+    *has_dup = 0;
+    if (n < 2) return MF_OK;
+    const int T = host_threads(), R = bucket_bits(n);
+    auto bucket = [&](int64_t p) {
+        return (int)(mix64((uint64_t)a[p] * 0x9E3779B97F4A7C15ull ^ (uint64_t)b[p]) >> (64 - R));
+    };
+    std::vector<int64_t> start;
+    std::unique_ptr<std::pair<int64_t, int64_t>[]> pr;
+    try {
+        pr.reset(new std::pair<int64_t, int64_t>[(size_t)n]);
+        partition_rows(n, R, T, bucket, start,
+                       [&](int64_t d, int64_t p) { pr[(size_t)d] = {a[p], b[p]}; });
+    } catch (const std::bad_alloc&) {
+        set_error("mf_pairs_duplicated: cannot allocate %lld rows", (long long)n);
+        return MF_ERR_NOMEM;
+    }
+    std::atomic<int> found{0};
+    for_buckets(1 << R, T, [&](int k) {
+        const auto* v = pr.get() + start[k];
+        const int64_t m = start[k + 1] - start[k];
+        size_t cap = 16;
+        while (cap < (size_t)m * 2) cap <<= 1;
+        struct Ent {
+            int64_t a, b;
+            bool used;
+        };
+        std::vector<Ent> table(cap, Ent{0, 0, false});
+        for (int64_t q = 0; q < m; ++q) {
+            size_t h = (size_t)(mix64((uint64_t)v[q].first ^ mix64((uint64_t)v[q].second)) &
+                                (cap - 1));
+            for (;; h = (h + 1) & (cap - 1)) {
+                Ent& e = table[h];
+                if (!e.used) {
+                    e = Ent{v[q].first, v[q].second, true};
+                    break;
+                }
+                if (e.a == v[q].first && e.b == v[q].second) {
+                    found.store(1);
+                    return;
+                }
+            }
+        }
+    }, &found);
+    *has_dup = found.load();
+    return MF_OK;
+}
+
+extern "C" int mf_factorize(const int64_t* vals, int64_t n, int64_t* codes, int64_t* uniques,
+                            int64_t* n_uniques) {
+    if (n < 0 || !n_uniques || (n > 0 && (!vals || !codes || !uniques))) {
+        set_error("mf_factorize: bad arguments");
+        return MF_ERR_INVALID;
+    }
+    *n_uniques = 0;
+    if (n == 0) return MF_OK;
+    const int T = host_threads(), R = bucket_bits(n), NB = 1 << R;
+    auto bucket = [&](int64_t p) { return (int)(mix64((uint64_t)vals[p]) >> (64 - R)); };
+    const int64_t nw = (n + 63) >> 6;
+    // uninitialised (first touched by the threads that fill them)
+    std::unique_ptr<int64_t[]> slot, sval, lid;
+    std::vector<int64_t> start, wpre;
+    std::vector<std::vector<int64_t>> first((size_t)NB);
+    std::unique_ptr<std::atomic<uint64_t>[]> bits;
+    try {
+        slot.reset(new int64_t[(size_t)n]);
+        sval.reset(new int64_t[(size_t)n]);
+        lid.reset(new int64_t[(size_t)n]);
+        partition_rows(n, R, T, bucket, start, [&](int64_t d, int64_t p) {
+            slot[d] = p;
+            sval[d] = vals[p];
+        });
+        wpre.resize((size_t)nw + 1);
+        bits.reset(new std::atomic<uint64_t>[(size_t)nw]);
+    } catch (const std::bad_alloc&) {
+        set_error("mf_factorize: cannot allocate %lld rows", (long long)n);
+        return MF_ERR_NOMEM;
+    }
+    parallel_chunks(nw, T, [&](int, int64_t lo, int64_t hi) {
+        for (int64_t w = lo; w < hi; ++w) bits[w].store(0, std::memory_order_relaxed);
+    });
+    // 1. per bucket (rows ascending): local ids in first-appearance order and
+    //    the row of each one's first appearance, marked in `bits`
+    for_buckets(NB, T, [&](int k) {
+        const int64_t m = start[k + 1] - start[k];
+        const int64_t* s = slot.get() + start[k];
+        const int64_t* sv = sval.get() + start[k];
+        int64_t* l = lid.get() + start[k];
+        size_t cap = 16;
+        while (cap < (size_t)m * 2) cap <<= 1;
+        struct Ent {
+            int64_t val, id;  // id -1 = empty
+        };
+        std::vector<Ent> table(cap, Ent{0, -1});
+        std::vector<int64_t>& f = first[(size_t)k];
+        for (int64_t q = 0; q < m; ++q) {
+            const int64_t v = sv[q];
+            size_t h = (size_t)(mix64((uint64_t)v) & (cap - 1));
+            for (;;) {
+                Ent& e = table[h];
+                if (e.id < 0) {
+                    e.val = v;
+                    e.id = l[q] = (int64_t)f.size();
+                    f.push_back(s[q]);
+                    bits[s[q] >> 6].fetch_or(1ull << (s[q] & 63), std::memory_order_relaxed);
+                    break;
+                }
+                if (e.val == v) {
+                    l[q] = e.id;
+                    break;
+                }
+                h = (h + 1) & (cap - 1);
+            }
+        }
+    });
+    // 2. code of a value = number of first appearances before its own
+    wpre[0] = 0;
+    for (int64_t w = 0; w < nw; ++w)
+        wpre[w + 1] = wpre[w] + __builtin_popcountll(bits[w].load(std::memory_order_relaxed));
+    const int64_t U = wpre[nw];
+    auto code_of_row = [&](int64_t row) {
+        const uint64_t word = bits[row >> 6].load(std::memory_order_relaxed);
+        return wpre[row >> 6] + __builtin_popcountll(word & ((1ull << (row & 63)) - 1));
+    };
+    // 3. scatter codes, write the uniques in code order
+    for_buckets(NB, T, [&](int k) {
+        std::vector<int64_t>& f = first[(size_t)k];
+        for (int64_t& row : f) {
+            const int64_t c = code_of_row(row);
+            uniques[c] = vals[row];
+            row = c;  // local id -> code
+        }
+        const int64_t m = start[k + 1] - start[k];
+        const int64_t* s = slot.get() + start[k];
+        const int64_t* l = lid.get() + start[k];
+        for (int64_t q = 0; q < m; ++q) codes[s[q]] = f[(size_t)l[q]];
+    });
+    *n_uniques = U;
+    return MF_OK;
+}
+
+extern "C" int mf_gather(const void* src, int64_t n_src, int32_t elem_bytes, const int64_t* idx,
+                         int64_t n, void* dst) {
+    if (n < 0 || n_src < 0 || (elem_bytes != 4 && elem_bytes != 8) ||
+        (n > 0 && (!src || !idx || !dst))) {
+        set_error("mf_gather: bad arguments");
+        return MF_ERR_INVALID;
+    }
+    std::atomic<int> bad{0};
+    auto run = [&](auto tag) {
+        using E = decltype(tag);
+        const E* s = static_cast<const E*>(src);
+        E* d = static_cast<E*>(dst);
+        parallel_chunks(n, host_threads(), [&](int, int64_t lo, int64_t hi) {
+            constexpr int kAhead = 16;
+            for (int64_t p = lo; p < hi; ++p) {
+                if (p + kAhead < hi) {
+                    const int64_t q = idx[p + kAhead];
+                    if (q >= 0 && q < n_src) __builtin_prefetch(s + q, 0, 0);
+                }
+                const int64_t q = idx[p];
+                if (q < 0 || q >= n_src) {
+                    bad.store(1);
+                    return;
+                }
+                d[p] = s[q];
+            }
+        });
+    };
+    if (elem_bytes == 4)
+        run(uint32_t{});
+    else
+        run(uint64_t{});
+    if (bad.load()) {
+        set_error("mf_gather: index outside [0, %lld)", (long long)n_src);
+        return MF_ERR_INVALID;
+    }
+    return MF_OK;
+}

@@ -1,0 +1,95 @@
+"""Host helpers of fit()'s preprocessing at 10^8 rows (mf_prep.cpp).
+
+``RecommenderBase._preprocess_data`` (recommender_base.py:120-141 of the
+reference) and the per-epoch row shuffle of ``_sgd``
+(kernel_matrix_factorization.py:371) cost seconds to a minute at C3 scale in
+pandas / NumPy, against ~12 ms per GPU epoch.  Each helper here returns what
+the pandas / NumPy call it replaces returns, and draws from NumPy's global
+legacy RandomState exactly as that call does (tests/test_prep.py compares
+them on the same seeds).
+"""
+
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+
+_MAX_N = (1 << 32) + 1       # NumPy's 32-bit random_interval branch
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def legacy_shuffle_(a: np.ndarray) -> None:
+    """``np.random.shuffle(a)`` for a 1-D contiguous 8-byte array, in place,
+    advancing the global RandomState exactly as NumPy does."""
+    if a.ndim != 1 or a.dtype.itemsize != 8 or not a.flags.c_contiguous \
+            or not a.flags.writeable or len(a) > _MAX_N:
+        np.random.shuffle(a)
+        return
+    st = np.random.get_state()
+    if st[0] != "MT19937":                       # pragma: no cover - legacy is MT19937
+        np.random.shuffle(a)
+        return
+    key = np.ascontiguousarray(st[1], dtype=np.uint32).copy()
+    pos = ctypes.c_int32(int(st[2]))
+    _lib.call("mf_legacy_shuffle", _ptr(key), ctypes.addressof(pos),
+              _ptr(a.view(np.int64)), len(a))
+    np.random.set_state(("MT19937", key, pos.value, st[3], st[4]))
+
+
+def legacy_permutation(n: int) -> np.ndarray:
+    """``np.random.permutation(n)`` (int64), same draws."""
+    perm = np.arange(n, dtype=np.int64)
+    legacy_shuffle_(perm)
+    return perm
+
+
+def as_int64_ids(col: np.ndarray):
+    """The id column as int64 (a view or a widening copy) when its values can
+    be hashed as 64-bit integers with equality preserved, else None."""
+    col = np.asarray(col)
+    if col.ndim != 1 or col.dtype.kind not in "iu":
+        return None
+    if col.dtype.itemsize == 8:
+        return np.ascontiguousarray(col).view(np.int64)
+    return col.astype(np.int64)
+
+
+def pairs_duplicated(a: np.ndarray, b: np.ndarray) -> bool:
+    """``DataFrame({a, b}).duplicated().sum() != 0`` for int64 id columns."""
+    a = np.ascontiguousarray(a, dtype=np.int64)
+    b = np.ascontiguousarray(b, dtype=np.int64)
+    if len(a) != len(b):
+        raise ValueError("id columns differ in length")
+    flag = ctypes.c_int32(0)
+    _lib.call("mf_pairs_duplicated", _ptr(a), _ptr(b), len(a), ctypes.addressof(flag))
+    return bool(flag.value)
+
+
+def factorize(vals: np.ndarray):
+    """``pd.factorize(vals, sort=False)`` for an int64 column: (codes int64,
+    uniques int64 in first-appearance order)."""
+    vals = np.ascontiguousarray(vals, dtype=np.int64)
+    codes = np.empty(len(vals), np.int64)
+    uniques = np.empty(len(vals), np.int64)
+    nu = ctypes.c_int64(0)
+    _lib.call("mf_factorize", _ptr(vals), len(vals), _ptr(codes), _ptr(uniques),
+              ctypes.addressof(nu))
+    return codes, uniques[: nu.value].copy()
+
+
+def gather(src: np.ndarray, idx: np.ndarray) -> np.ndarray:
+    """``src[idx]`` for a 1-D array of 4- or 8-byte elements (threaded)."""
+    src = np.ascontiguousarray(src)
+    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    if src.ndim != 1 or src.dtype.itemsize not in (4, 8) or src.dtype.hasobject:
+        return src[idx]
+    dst = np.empty(len(idx), src.dtype)
+    _lib.call("mf_gather", _ptr(src), len(src), src.dtype.itemsize, _ptr(idx), len(idx),
+              _ptr(dst))
+    return dst

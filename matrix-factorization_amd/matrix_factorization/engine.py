@@ -31,7 +31,7 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from . import _lib
+from . import _lib, _prep
 
 _VOID = ctypes.c_void_p
 
@@ -687,7 +687,7 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
     train_rmse = []
     for epoch in range(n_epochs):
         if schedule == "exact":
-            np.random.shuffle(order)
+            _prep.legacy_shuffle_(order)          # = np.random.shuffle(order)
             engine.epoch_exact(order, lr, reg, update_user, update_item)
         elif schedule == "colored":
             seq = np.random.permutation(nb).astype(np.int32)

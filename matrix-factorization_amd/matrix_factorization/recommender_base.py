@@ -17,6 +17,12 @@ import numpy as np
 import pandas as pd
 from sklearn.base import BaseEstimator, RegressorMixin
 
+from . import _prep
+
+# integer id columns of at least this many rows take the native
+# preprocessing path (mf_prep.cpp); results are identical either way
+FAST_PREP_MIN_ROWS = 1 << 16
+
 
 def _index_of(keys) -> pd.Index:
     return pd.Index(list(keys))
@@ -81,9 +87,18 @@ class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
             X["rating"] = y
 
         if type in ("fit", "update"):
-            if X.duplicated(subset=["user_id", "item_id"]).sum() != 0:
-                raise ValueError("Duplicate user-item ratings in matrix")
-            X = X.sample(frac=1, replace=False)
+            ids = self._int64_ids(X)
+            if ids is not None:
+                if _prep.pairs_duplicated(*ids):
+                    raise ValueError("Duplicate user-item ratings in matrix")
+                perm = _prep.legacy_permutation(len(X))       # = X.sample's draw
+                if type == "fit":
+                    return self._fit_maps_native(X, ids, perm)
+                X = X.iloc[perm]
+            else:
+                if X.duplicated(subset=["user_id", "item_id"]).sum() != 0:
+                    raise ValueError("Duplicate user-item ratings in matrix")
+                X = X.sample(frac=1, replace=False)
 
         if type == "fit":
             ucodes, uniq_u = pd.factorize(X["user_id"], sort=False)
@@ -117,6 +132,42 @@ class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
         if type == "update":
             return out, known_users, new_users
         return out
+
+    @staticmethod
+    def _int64_ids(X: pd.DataFrame):
+        """(user ids, item ids) as int64 arrays when both columns are integer
+        and the frame is large enough for the native path, else None."""
+        if len(X) < FAST_PREP_MIN_ROWS:
+            return None
+        u = _prep.as_int64_ids(X["user_id"].to_numpy())
+        i = _prep.as_int64_ids(X["item_id"].to_numpy())
+        return None if u is None or i is None else (u, i)
+
+    def _fit_maps_native(self, X: pd.DataFrame, ids, perm: np.ndarray) -> pd.DataFrame:
+        """The fit branch for integer ids: the rows in ``perm`` order (the
+        order X.sample(frac=1) gives), id maps in first-appearance order of
+        that order (pd.factorize / unique of the shuffled column), all in
+        mf_prep.cpp."""
+        maps = []
+        codes = []
+        for col, v in zip(("user_id", "item_id"), ids):
+            c, uniq = _prep.factorize(_prep.gather(v, perm))
+            dt = X[col].dtype
+            uniq = uniq.view(dt) if dt.itemsize == 8 else uniq.astype(dt)
+            maps.append(dict(zip(uniq, range(len(uniq)))))
+            codes.append(c)
+        self.user_id_map, self.item_id_map = maps
+        self.n_users, self.n_items = len(maps[0]), len(maps[1])
+        rating = X["rating"].to_numpy()
+        rating = _prep.gather(rating, perm) if rating.dtype.kind in "fiu" else rating[perm]
+        idx = X.index
+        if isinstance(idx, pd.RangeIndex):
+            idx = pd.Index(idx.start + idx.step * perm if (idx.start, idx.step) != (0, 1)
+                           else perm)
+        else:
+            idx = idx.take(perm)
+        return pd.DataFrame({"user_id": codes[0], "item_id": codes[1], "rating": rating},
+                            index=idx, copy=False)
 
     @abstractmethod
     def fit(self, X: pd.DataFrame, y: pd.Series):

@@ -1,0 +1,174 @@
+"""fit() preprocessing on the native path (mf_prep.cpp, host only) against the
+pandas / NumPy calls it replaces (recommender_base.py:120-141 and
+kernel_matrix_factorization.py:371 of the reference): same outputs, same
+draws from NumPy's global RandomState, same errors.  CPU only."""
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from matrix_factorization import _lib, _prep
+from matrix_factorization import recommender_base as rb
+from matrix_factorization import KernelMF
+
+
+def _state_equal(s1, s2):
+    return (s1[0] == s2[0] and np.array_equal(s1[1], s2[1]) and s1[2] == s2[2]
+            and s1[3] == s2[3] and s1[4] == s2[4])
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 5, 64, 65, 1000, 70_001, 1_000_003])
+def test_legacy_permutation_is_numpys(n):
+    for seed in (0, 11):
+        np.random.seed(seed)
+        a = np.random.permutation(n)
+        s1 = np.random.get_state()
+        np.random.seed(seed)
+        b = _prep.legacy_permutation(n)
+        s2 = np.random.get_state()
+        assert np.array_equal(a, b)
+        assert _state_equal(s1, s2)
+
+
+def test_legacy_shuffle_mid_stream():
+    # a pending Gaussian and an MT position inside the 624-word block
+    for draws in (0, 1, 623, 624, 625, 5000):
+        np.random.seed(7)
+        np.random.randint(0, 10, draws)
+        np.random.normal()
+        st = np.random.get_state()
+        a = np.arange(123_457, dtype=np.int64) * 3
+        np.random.shuffle(a)
+        x1 = np.random.rand(3)
+        np.random.set_state(st)
+        b = np.arange(123_457, dtype=np.int64) * 3
+        _prep.legacy_shuffle_(b)
+        x2 = np.random.rand(3)
+        assert np.array_equal(a, b) and np.array_equal(x1, x2), draws
+
+
+def test_legacy_shuffle_falls_back_for_other_layouts():
+    np.random.seed(3)
+    a = np.arange(1000, dtype=np.int32)
+    np.random.shuffle(a)
+    np.random.seed(3)
+    b = np.arange(1000, dtype=np.int32)
+    _prep.legacy_shuffle_(b)
+    assert np.array_equal(a, b)
+
+
+def test_legacy_shuffle_rejects_bad_state():
+    key = np.zeros(624, np.uint32)
+    import ctypes
+    pos = ctypes.c_int32(625)
+    a = np.arange(10, dtype=np.int64)
+    with pytest.raises(_lib.MFLibraryError):
+        _lib.call("mf_legacy_shuffle", key.ctypes.data, ctypes.addressof(pos), a.ctypes.data, 10)
+
+
+@pytest.mark.parametrize("n,hi", [(0, 5), (1, 5), (10, 3), (5000, 40), (200_000, 10**15),
+                                  (300_000, 2**62), (1_000_000, 700)])
+def test_factorize_is_pandas(n, hi):
+    rs = np.random.RandomState(n % 1000)
+    v = rs.randint(-hi, hi, n).astype(np.int64)
+    c, u = _prep.factorize(v)
+    c2, u2 = pd.factorize(v, sort=False)
+    assert np.array_equal(c, c2) and np.array_equal(u, u2)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 1000, 300_000])
+def test_pairs_duplicated_is_pandas(n):
+    rs = np.random.RandomState(n)
+    side = max(2, int(np.sqrt(n)) * 3)
+    a = rs.randint(0, side, n)
+    b = rs.randint(0, side, n)
+    want = bool(pd.DataFrame({"a": a, "b": b}).duplicated().sum() != 0)
+    assert _prep.pairs_duplicated(a, b) == want
+    k = np.unique(a.astype(np.int64) * side + b)
+    rs.shuffle(k)
+    assert not _prep.pairs_duplicated(k // side, k % side)
+    if len(k) > 1:                                # one duplicate at the far end
+        k2 = np.concatenate([k, k[:1]])
+        assert _prep.pairs_duplicated(k2 // side, k2 % side)
+    # (a, b) and (b, a) are different pairs
+    assert not _prep.pairs_duplicated(np.array([1, 2]), np.array([2, 1]))
+
+
+def test_gather_and_bounds():
+    rs = np.random.RandomState(0)
+    for dt in (np.float32, np.float64, np.int32, np.int64):
+        src = rs.randint(0, 1000, 100_000).astype(dt)
+        idx = rs.randint(0, len(src), 250_000)
+        assert np.array_equal(_prep.gather(src, idx), src[idx])
+    with pytest.raises(_lib.MFLibraryError):
+        _prep.gather(np.zeros(10, np.float32), np.array([0, 10]))
+
+
+def _frame(n, dtype, seed, index=None):
+    rs = np.random.RandomState(seed)
+    nu, ni = 3000, 700
+    keys = rs.choice(nu * ni, n, replace=False)
+    if np.dtype(dtype).kind == "i":
+        u = (keys // ni * 7 - 5000).astype(dtype)
+    elif np.dtype(dtype).itemsize == 8:           # ids above 2^63
+        u = (keys // ni).astype(np.uint64) + np.uint64(2**63)
+    else:
+        u = (keys // ni + 7).astype(dtype)
+    i = (keys % ni * 13 + 1).astype(dtype)
+    X = pd.DataFrame({"user_id": u, "item_id": i, "extra": 1.0}, index=index)
+    y = pd.Series(rs.randint(1, 6, n).astype(np.float64), index=X.index)
+    return X, y
+
+
+def _run(model, X, y, typ, fast, monkeypatch, seed):
+    monkeypatch.setattr(rb, "FAST_PREP_MIN_ROWS", 0 if fast else 1 << 62)
+    np.random.seed(seed)
+    out = model._preprocess_data(X, y, type=typ)
+    return out, np.random.get_state()
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.int64, np.uint32, np.uint64])
+@pytest.mark.parametrize("index", ["range", "offset", "labels"])
+def test_fit_preprocess_native_equals_pandas(dtype, index, monkeypatch):
+    n = 20_000
+    idx = {"range": None, "offset": pd.RangeIndex(5, 5 + 3 * n, 3),
+           "labels": pd.Index(np.random.RandomState(1).permutation(n) * 2 + 1)}[index]
+    X, y = _frame(n, dtype, 4, idx)
+    ma, mb = KernelMF(), KernelMF()
+    a, sa = _run(ma, X, y, "fit", True, monkeypatch, 21)
+    b, sb = _run(mb, X, y, "fit", False, monkeypatch, 21)
+    assert _state_equal(sa, sb)
+    assert list(a.columns) == list(b.columns)
+    assert a.index.equals(b.index)
+    for c in ("user_id", "item_id", "rating"):
+        assert a[c].dtype == b[c].dtype and np.array_equal(a[c].to_numpy(), b[c].to_numpy())
+    assert (ma.n_users, ma.n_items) == (mb.n_users, mb.n_items)
+    assert list(ma.user_id_map.items()) == list(mb.user_id_map.items())
+    assert list(ma.item_id_map.items()) == list(mb.item_id_map.items())
+    # the reference's own construction: unique() of the shuffled frame
+    np.random.seed(21)
+    Xs = X.loc[:, ["user_id", "item_id"]].sample(frac=1, replace=False)
+    assert list(ma.user_id_map) == list(Xs["user_id"].unique())
+    assert list(ma.item_id_map) == list(Xs["item_id"].unique())
+
+
+@pytest.mark.parametrize("fast", [True, False])
+def test_duplicates_raise(fast, monkeypatch):
+    X, y = _frame(5000, np.int64, 2)
+    X.iloc[4000, :2] = X.iloc[17, :2].to_numpy()
+    st = np.random.get_state()
+    with pytest.raises(ValueError, match="Duplicate"):
+        _run(KernelMF(), X, y, "fit", fast, monkeypatch, 0)
+    np.random.set_state(st)
+
+
+def test_update_preprocess_native_equals_pandas(monkeypatch):
+    X, y = _frame(8000, np.int64, 5)
+    ma, mb = KernelMF(), KernelMF()
+    _run(ma, X.iloc[:6000], y.iloc[:6000], "fit", True, monkeypatch, 1)
+    _run(mb, X.iloc[:6000], y.iloc[:6000], "fit", False, monkeypatch, 1)
+    Xn, yn = X.iloc[5000:], y.iloc[5000:]
+    (a, ka, na), sa = _run(ma, Xn, yn, "update", True, monkeypatch, 2)
+    (b, kb, nb), sb = _run(mb, Xn, yn, "update", False, monkeypatch, 2)
+    assert _state_equal(sa, sb) and a.equals(b) and ka == kb and na == nb
+    assert list(ma.user_id_map.items()) == list(mb.user_id_map.items())
