@@ -33,37 +33,20 @@
 #include <vector>
 
 #include "../../include/mf_hip.h"
+#include "mf_host.hpp"
 
 namespace mf {
 void set_error(const char* fmt, ...);
 }
+using mf::bucket_bits;
+using mf::for_buckets;
+using mf::host_threads;
+using mf::mix64;
+using mf::parallel_chunks;
+using mf::partition_rows;
 using mf::set_error;
 
 namespace {
-
-int host_threads() {
-    if (const char* s = std::getenv("MF_HOST_THREADS")) {
-        const int v = std::atoi(s);
-        if (v > 0) return std::min(v, 256);
-    }
-    const unsigned hw = std::thread::hardware_concurrency();
-    return (int)std::max(1u, std::min(16u, hw));
-}
-
-// fn(t, lo, hi) over [0, n) cut into T contiguous chunks
-void parallel_chunks(int64_t n, int T, const std::function<void(int, int64_t, int64_t)>& fn) {
-    if (T <= 1 || n < (int64_t)1 << 16) {
-        fn(0, 0, n);
-        return;
-    }
-    std::vector<std::thread> th;
-    th.reserve(T);
-    for (int t = 0; t < T; ++t) {
-        const int64_t lo = n * t / T, hi = n * (t + 1) / T;
-        th.emplace_back(fn, t, lo, hi);
-    }
-    for (auto& x : th) x.join();
-}
 
 // ---------------------------------------------------------------- MT19937
 // The standard Mersenne Twister (Matsumoto & Nishimura 1998) as NumPy's
@@ -161,70 +144,6 @@ extern "C" int mf_legacy_shuffle(uint32_t* mt_key, int32_t* mt_pos, int64_t* dat
     return MF_OK;
 }
 
-namespace {
-
-int bucket_bits(int64_t n) {  // 2^R buckets of <= ~16K entries
-    int R = 1;
-    while (R < 16 && (n >> R) > (1 << 14)) ++R;
-    return R;
-}
-
-inline uint64_t mix64(uint64_t x) {  // splitmix64 finaliser
-    x ^= x >> 30;
-    x *= 0xbf58476d1ce4e5b9ull;
-    x ^= x >> 27;
-    x *= 0x94d049bb133111ebull;
-    return x ^ (x >> 31);
-}
-
-// Stable hash partition of rows [0, n) into 2^R buckets: bucket b owns the
-// destinations start[b] .. start[b+1], filled in ascending row order (chunk t
-// precedes chunk t+1 and each chunk is scattered in order) by emit(dst, row).
-template <class F, class E>
-void partition_rows(int64_t n, int R, int T, F bucket, std::vector<int64_t>& start, E emit) {
-    const int NB = 1 << R;
-    const int Tused = (T <= 1 || n < (int64_t)1 << 16) ? 1 : T;
-    std::vector<int64_t> count((size_t)Tused * NB, 0);
-    parallel_chunks(n, Tused, [&](int t, int64_t lo, int64_t hi) {
-        int64_t* c = count.data() + (size_t)t * NB;
-        for (int64_t p = lo; p < hi; ++p) ++c[bucket(p)];
-    });
-    start.assign((size_t)NB + 1, 0);
-    int64_t acc = 0;
-    for (int b = 0; b < NB; ++b) {
-        start[b] = acc;
-        for (int t = 0; t < Tused; ++t) {
-            int64_t& c = count[(size_t)t * NB + b];
-            const int64_t v = c;
-            c = acc;  // write cursor of chunk t in bucket b
-            acc += v;
-        }
-    }
-    start[NB] = acc;
-    parallel_chunks(n, Tused, [&](int t, int64_t lo, int64_t hi) {
-        int64_t* cur = count.data() + (size_t)t * NB;
-        for (int64_t p = lo; p < hi; ++p) emit(cur[bucket(p)]++, p);
-    });
-}
-
-// fn(b) for every bucket b, dynamically balanced over T threads; stops early
-// once `stop` is set
-template <class F>
-void for_buckets(int NB, int T, F fn, const std::atomic<int>* stop = nullptr) {
-    std::atomic<int> next{0};
-    auto work = [&]() {
-        for (int b; !(stop && stop->load(std::memory_order_relaxed)) &&
-                    (b = next.fetch_add(1)) < NB;)
-            fn(b);
-    };
-    std::vector<std::thread> th;
-    for (int t = 1; t < std::min(T, NB); ++t) th.emplace_back(work);
-    work();
-    for (auto& x : th) x.join();
-}
-
-}  // namespace
-
 extern "C" int mf_pairs_duplicated(const int64_t* a, const int64_t* b, int64_t n,
                                    int32_t* has_dup) {
     if (!has_dup || n < 0 || (n > 0 && (!a || !b))) {
@@ -241,7 +160,7 @@ extern "C" int mf_pairs_duplicated(const int64_t* a, const int64_t* b, int64_t n
     std::unique_ptr<std::pair<int64_t, int64_t>[]> pr;
     try {
         pr.reset(new std::pair<int64_t, int64_t>[(size_t)n]);
-        partition_rows(n, R, T, bucket, start,
+        partition_rows(n, 1 << R, T, bucket, start,
                        [&](int64_t d, int64_t p) { pr[(size_t)d] = {a[p], b[p]}; });
     } catch (const std::bad_alloc&) {
         set_error("mf_pairs_duplicated: cannot allocate %lld rows", (long long)n);
@@ -298,7 +217,7 @@ extern "C" int mf_factorize(const int64_t* vals, int64_t n, int64_t* codes, int6
         slot.reset(new int64_t[(size_t)n]);
         sval.reset(new int64_t[(size_t)n]);
         lid.reset(new int64_t[(size_t)n]);
-        partition_rows(n, R, T, bucket, start, [&](int64_t d, int64_t p) {
+        partition_rows(n, 1 << R, T, bucket, start, [&](int64_t d, int64_t p) {
             slot[d] = p;
             sval[d] = vals[p];
         });

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "../../include/mf_hip.h"
+#include "mf_host.hpp"
 
 namespace mf {
 
@@ -210,20 +211,27 @@ extern "C" int mf_sched_slices(const int32_t* user_ids, const int32_t* item_ids,
     }
     if (int rc = check_ids(user_ids, item_ids, n, n_users, n_items)) return rc;
     try {
-        // stable counting sort by key = slice(item) * n_users + user
-        const int64_t nkeys = (int64_t)n_slices * n_users;
-        std::vector<int64_t> cnt((size_t)nkeys + 1, 0);
+        // stable sort by key = slice(item) * n_users + user: a stable
+        // partition by slice, then a counting sort by user inside each slice
         auto slice_of = [&](int32_t it) {
-            return (int64_t)((int64_t)it * n_slices / (n_items > 0 ? n_items : 1));
+            return (int)((int64_t)it * n_slices / (n_items > 0 ? n_items : 1));
         };
-        for (int64_t j = 0; j < n; ++j)
-            cnt[slice_of(item_ids[j]) * n_users + user_ids[j] + 1] += 1;
-        for (int64_t q = 0; q < nkeys; ++q) cnt[q + 1] += cnt[q];
-        for (int32_t x = 0; x <= n_slices; ++x) slice_offsets[x] = cnt[(int64_t)x * n_users];
-        for (int64_t j = 0; j < n; ++j) {
-            const int64_t key = slice_of(item_ids[j]) * n_users + user_ids[j];
-            sched_out[cnt[key]++] = (int32_t)j;
-        }
+        const int T = mf::host_threads();
+        std::vector<int64_t> start;
+        mf::partition_rows(
+            n, n_slices, T, [&](int64_t p) { return slice_of(item_ids[p]); }, start,
+            [&](int64_t d, int64_t p) { sched_out[d] = (int32_t)p; });
+        for (int32_t x = 0; x <= n_slices; ++x) slice_offsets[x] = start[x];
+        mf::for_buckets(n_slices, T, [&](int s) {
+            int32_t* q = sched_out + start[s];
+            const int64_t m = start[s + 1] - start[s];
+            std::vector<int64_t> cnt((size_t)n_users + 1, 0);
+            for (int64_t j = 0; j < m; ++j) cnt[user_ids[q[j]] + 1] += 1;
+            for (int32_t x = 0; x < n_users; ++x) cnt[x + 1] += cnt[x];
+            std::vector<int32_t> tmp((size_t)m);
+            for (int64_t j = 0; j < m; ++j) tmp[cnt[user_ids[q[j]]]++] = q[j];
+            std::copy(tmp.begin(), tmp.end(), q);
+        });
     } catch (const std::bad_alloc&) {
         set_error("mf_sched_slices: out of host memory");
         return MF_ERR_NOMEM;

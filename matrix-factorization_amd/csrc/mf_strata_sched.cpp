@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/mf_hip.h"
+#include "mf_host.hpp"
 
 namespace mf {
 void set_error(const char* fmt, ...);
@@ -181,24 +182,38 @@ extern "C" int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item
         for (int32_t x = item_bounds[b]; x < item_bounds[b + 1]; ++x) ib_of[x] = b;
     }
     const int64_t BB = (int64_t)B * B;
-    std::vector<int32_t> key(n), bucket(n);
-    std::vector<int64_t> pos(BB + 1, 0);
-    for (int64_t j = 0; j < n; ++j) {
-        const int32_t uu = user_ids[j], ii = item_ids[j];
-        if (uu < 0 || uu >= n_users || ii < 0 || ii >= n_items) {
-            set_error("rating %lld has ids (%d, %d) outside [0,%d) x [0,%d)", (long long)j, uu, ii,
-                      n_users, n_items);
+    const int T = mf::host_threads();
+    {   // first rating (lowest index) with an id out of range, if any
+        std::atomic<int64_t> first_bad{n};
+        mf::parallel_chunks(n, T, [&](int, int64_t lo, int64_t hi) {
+            for (int64_t j = lo; j < hi; ++j) {
+                const int32_t uu = user_ids[j], ii = item_ids[j];
+                if (uu < 0 || uu >= n_users || ii < 0 || ii >= n_items) {
+                    int64_t cur = first_bad.load();
+                    while (j < cur && !first_bad.compare_exchange_weak(cur, j)) {
+                    }
+                    return;
+                }
+            }
+        });
+        const int64_t j = first_bad.load();
+        if (j < n) {
+            set_error("rating %lld has ids (%d, %d) outside [0,%d) x [0,%d)", (long long)j,
+                      user_ids[j], item_ids[j], n_users, n_items);
             return MF_ERR_INVALID;
         }
-        const int32_t w = ib_of[ii];
-        const int32_t s = (ub_of[uu] - w + B) % B;
-        key[j] = (int32_t)((int64_t)s * B + w);
-        ++pos[key[j] + 1];
     }
-    for (int64_t b = 0; b < BB; ++b) pos[b + 1] += pos[b];
-    std::vector<int64_t> boff(pos);
-    for (int64_t j = 0; j < n; ++j) bucket[pos[key[j]]++] = (int32_t)j;
-    std::vector<int32_t>().swap(key);
+    // ratings by block (stable): block of (user range ub, item range w) is
+    // stored at s*B + w with s = (ub - w) mod B
+    std::vector<int32_t> bucket(n);
+    std::vector<int64_t> boff;
+    mf::partition_rows(
+        n, (int)BB, T,
+        [&](int64_t j) {
+            const int32_t w = ib_of[item_ids[j]];
+            return (int)((int64_t)((ub_of[user_ids[j]] - w + B) % B) * B + w);
+        },
+        boff, [&](int64_t d, int64_t j) { bucket[d] = (int32_t)j; });
 
     // plan the blocks in chunks of 64 on worker threads
     const int64_t CH = 64;

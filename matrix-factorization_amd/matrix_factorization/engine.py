@@ -167,15 +167,21 @@ class StrataPlan:
         self.max_users = int(np.diff(ubnd).max()) if B else 0
 
     def to_device(self, u, i, r, dev) -> None:
-        """Upload the bounds, the step offsets and the triples in plan order
-        (idle slots: user -1, item -1, rating 0)."""
+        """Upload the bounds and the step offsets; lay the triples out in plan
+        order (idle slots: user -1, item -1, rating 0).  u / i / r are the
+        triples in original order, host arrays or tensors already on ``dev``
+        (then the reordering happens on the device)."""
         to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         self.d_ubnd, self.d_ibnd, self.d_bstep = to(self.ubnd), to(self.ibnd), to(self.bstep)
-        valid = self.sched >= 0
-        idx = np.where(valid, self.sched, 0)
-        self.d_u = to(np.where(valid, u[idx], -1).astype(np.int32))
-        self.d_i = to(np.where(valid, i[idx], -1).astype(np.int32))
-        self.d_r = to(np.where(valid, r[idx], 0).astype(r.dtype))
+        u, i, r = (x if isinstance(x, torch.Tensor) else torch.from_numpy(
+            np.ascontiguousarray(x)).to(dev) for x in (u, i, r))
+        sched = to(self.sched)
+        valid = sched >= 0
+        idx = torch.where(valid, sched, 0).long()
+        del sched
+        self.d_u = torch.where(valid, u.index_select(0, idx), -1).to(torch.int32)
+        self.d_i = torch.where(valid, i.index_select(0, idx), -1).to(torch.int32)
+        self.d_r = torch.where(valid, r.index_select(0, idx), 0).to(r.dtype)
 
     @property
     def n_positions(self) -> int:
@@ -335,9 +341,13 @@ class SGDEngine:
             return
         sched, offs = sched_slices(self.u_host, self.i_host, self.n_users, self.n_items,
                                    N_SLICES)
-        self.eu = torch.from_numpy(self.u_host[sched]).to(self.dev)
-        self.ei = torch.from_numpy(self.i_host[sched]).to(self.dev)
-        self.er = torch.from_numpy(self.r_host[sched]).to(self.dev)
+        # reorder on the device from the uploaded triples (one int32 upload
+        # instead of three host gathers of n elements)
+        d_sched = torch.from_numpy(sched).to(self.dev).long()
+        self.eu = self.u.index_select(0, d_sched)
+        self.ei = self.i.index_select(0, d_sched)
+        self.er = self.r.index_select(0, d_sched)
+        del d_sched
         self.eval_offs = offs
 
     def _dev(self, a, shape) -> torch.Tensor:
@@ -403,7 +413,7 @@ class SGDEngine:
         sched, bstep = sched_strata(self.u_host, self.i_host, self.n_users, self.n_items, B,
                                     ub, ib, ns)
         plan = StrataPlan(B, ns, ub, ib, bstep, sched)
-        plan.to_device(self.u_host, self.i_host, self.r_host, self.dev)
+        plan.to_device(self.u, self.i, self.r, self.dev)
         self.strata = plan
         return plan
 

@@ -1,0 +1,81 @@
+"""Wall time of the public KernelMF.fit() at C3 scale, split by phase.
+
+Synthetic 1M x 100K, 100M ratings (bench.synth), rank 64, linear kernel,
+float32, strata schedule.  Phases are timed by wrapping the functions fit()
+calls (preprocessing, normal() initialisation is the remainder, engine
+upload + strata plan, SGD epochs incl. the RMSE passes, parameter download).
+Usage: python tools/fit_walltime.py [--epochs 20] [--nnz 100000000]
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "matrix-factorization_amd"))
+
+import numpy as np
+import pandas as pd
+import torch
+
+import bench
+from matrix_factorization import KernelMF
+from matrix_factorization import kernel_matrix_factorization as kmf
+from matrix_factorization import recommender_base as rb
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--epochs", type=int, default=20)
+    ap.add_argument("--nnz", type=int, default=100_000_000)
+    ap.add_argument("--users", type=int, default=1_000_000)
+    ap.add_argument("--items", type=int, default=100_000)
+    ap.add_argument("--pandas-prep", action="store_true",
+                    help="force the pandas preprocessing path (reference-shaped)")
+    args = ap.parse_args()
+    if args.pandas_prep:
+        rb.FAST_PREP_MIN_ROWS = 1 << 62
+    t0 = time.perf_counter()
+    u, i, r = bench.synth(args.users, args.items, args.nnz)
+    X = pd.DataFrame({"user_id": u, "item_id": i})
+    y = pd.Series(r.astype(np.float64))
+    del u, i, r
+    t_synth = time.perf_counter() - t0
+    phases = {}
+
+    def timed(name, fn):
+        def wrap(*a, **kw):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            out = fn(*a, **kw)
+            torch.cuda.synchronize()
+            phases[name] = phases.get(name, 0.0) + time.perf_counter() - t
+            return out
+        return wrap
+
+    KernelMF._preprocess_data = timed("preprocess", KernelMF._preprocess_data)
+    KernelMF._make_engine = timed("engine_upload", KernelMF._make_engine)
+    kmf.fit_epochs = timed("epochs_incl_plan", kmf.fit_epochs)
+    KernelMF._sync_params = timed("download", KernelMF._sync_params)
+    torch.zeros(1, device="cuda:0")
+    m = KernelMF(n_factors=64, n_epochs=args.epochs, lr=0.01, reg=0.02, verbose=0,
+                 min_rating=1, max_rating=5, dtype="float32", schedule="strata")
+    np.random.seed(0)
+    t = time.perf_counter()
+    m.fit(X, y)
+    total = time.perf_counter() - t
+    phases["init_normal_and_other"] = total - sum(phases.values())
+    print(json.dumps({"what": "KernelMF.fit wall time", "nnz": args.nnz,
+                      "n_users": m.n_users, "n_items": m.n_items, "epochs": args.epochs,
+                      "prep_path": "pandas" if args.pandas_prep else "native",
+                      "fit_s": round(total, 3),
+                      "phases_s": {k: round(v, 3) for k, v in phases.items()},
+                      "final_train_rmse": float(m.train_rmse[-1]),
+                      "synth_s": round(t_synth, 1)}))
+
+
+if __name__ == "__main__":
+    main()
