@@ -182,12 +182,15 @@ int32_t mf_strata_slots(int32_t n_factors, int32_t dtype);
  * slice_offsets (HOST, nullable, n_slices + 1 <= 17 entries): the ratings
  * are ordered by mf_sched_slices; slice x is walked by the workgroups
  * b % n_slices == x (XCD-local Q slices).  NULL = one slice.
+ * n_users / n_items: rows of user_features / item_features (every id must
+ * be below them).
  */
 size_t mf_sse_workspace_bytes(int64_t n_ratings);
 int mf_sse(const int32_t* user_ids, const int32_t* item_ids,
            const void* ratings, int64_t n_ratings, double global_mean,
            const void* user_biases, const void* item_biases,
            const void* user_features, const void* item_features,
+           int32_t n_users, int32_t n_items,
            int32_t n_factors, int32_t kernel, int32_t dtype, double gamma,
            double min_rating, double max_rating,
            const int64_t* slice_offsets, int32_t n_slices, void* workspace,

@@ -16,6 +16,7 @@
 #pragma once
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "mf_common.hpp"
@@ -105,6 +106,8 @@ struct ReadArgs {
     T* out;
     double* partials;
     Hyper<T> h;
+    // byte sizes of P, Q, Bu, Bi (buffer-load ranges of k_sse_owned; < 4 GiB)
+    uint64_t p_bytes, q_bytes, bu_bytes, bi_bytes;
 };
 
 // Work split of the read-only passes: `n` slices of the rating array (the
@@ -480,6 +483,143 @@ __global__ __launch_bounds__(kBlock) void k_sse_stream(ReadArgs<T> A, SliceTab S
     }
 }
 
+// Training SSE with user rows OWNED by lane groups (same result as
+// k_sse_stream up to the order of the FP64 accumulation).  The wave's share
+// of its slice is cut into R contiguous runs, one per group of GS lanes; in
+// mf_sched_slices order a run is user-major (a user has ~nnz/(n_users *
+// slices) consecutive ratings in a slice), so a group loads a user's P row
+// and bias once per run of that user and only the item row per rating: the
+// vector-memory instructions per rating drop from two row loads to one plus
+// the rare user change.  Each group walks its run S ratings per step; the
+// triples come in chunks of GS per group (lane l of group g holds rating
+// r0 + c + l), prefetched one chunk ahead.
+template <typename T, int W, int GS, int V, int KERN, int S>
+__global__ __launch_bounds__(kBlock) void k_sse_owned(ReadArgs<T> A, SliceTab SL) {
+    using VT = typename VecOf<T, W>::type;
+    constexpr int R = kWave / GS;
+    static_assert(GS % S == 0, "a chunk of GS ratings is whole steps");
+    const int lane = threadIdx.x & (kWave - 1);
+    const int g = lane / GS;
+    const int l = lane % GS;
+    const int k = A.k;
+    const int kv = k / W;
+    const Hyper<T> h = A.h;
+    const int x_slice = blockIdx.x % SL.n;
+    const int64_t bps = gridDim.x / SL.n;
+    const int64_t nw_slice = bps * kWavesPerBlock;
+    const int64_t wv = (int64_t)(blockIdx.x / SL.n) * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t s0 = SL.off[x_slice], len = SL.off[x_slice + 1] - s0;
+    const int64_t b0 = s0 + len * wv / nw_slice;
+    const int64_t b1 = s0 + len * (wv + 1) / nw_slice;
+    double acc = 0.0;
+    if (b0 < b1) {
+        const int64_t wl = b1 - b0;
+        const int64_t r0 = b0 + wl * g / R, r1 = b0 + wl * (g + 1) / R;   // this group's run
+        const int64_t maxrun = (wl + R - 1) / R;                          // wave-uniform trips
+        const int64_t last = r1 > r0 ? r1 - 1 : b0;
+        const __amdgpu_buffer_rsrc_t rp = buf_rsrc(A.P, A.p_bytes), rq = buf_rsrc(A.Q, A.q_bytes);
+        const __amdgpu_buffer_rsrc_t rbu = buf_rsrc(A.Bu, A.bu_bytes), rbi = buf_rsrc(A.Bi, A.bi_bytes);
+        auto fetch = [&](int64_t c, int& u, int& i, T& r) {
+            const int64_t j = min(r0 + c + l, last);
+            u = A.u[j]; i = A.i[j]; r = A.r[j];
+        };
+        int nu_, ni_;
+        T nr_;
+        fetch(0, nu_, ni_, nr_);
+        int pu = -1;                       // user whose row is held in pp / pbu
+        VT pp[V];
+        T pbu = (T)0;
+#pragma unroll
+        for (int v = 0; v < V; ++v) pp[v] = (VT)(T)0;
+        for (int64_t c = 0; c < maxrun; c += GS) {
+            const int tu = nu_, ti = ni_;
+            const T tr = nr_;
+            if (c + GS < maxrun) fetch(c + GS, nu_, ni_, nr_);          // prefetch
+#pragma unroll 1
+            for (int t = 0; t < GS; t += S) {
+                int uu[S], ii[S];
+                T rr[S];
+                bool hv[S], need[S];
+#pragma unroll
+                for (int x = 0; x < S; ++x) {
+                    const int src = g * GS + t + x;
+                    uu[x] = take_i<GS>(tu, src);
+                    ii[x] = take_i<GS>(ti, src);
+                    rr[x] = take_f<GS>(tr, src);
+                    hv[x] = r0 + c + t + x < r1;
+                }
+#pragma unroll
+                for (int x = 0; x < S; ++x) need[x] = uu[x] != (x == 0 ? pu : uu[x - 1]);
+                // Branch-free loads: item rows for every rating, user rows as
+                // buffer loads whose offset is out of range (returns 0, no
+                // memory access) where the run stays on the same user.
+                VT q[S][V], p[S][V];
+                T bi[S], bu[S];
+#pragma unroll
+                for (int x = 0; x < S; ++x) {
+#pragma unroll
+                    for (int v = 0; v < V; ++v) {
+                        const int vi = v * GS + l;
+                        const int vc = vi < kv ? vi : kv - 1;
+                        q[x][v] = buf_ld<0, VT>(rq, (uint32_t)(((uint32_t)ii[x] * (uint32_t)k +
+                                                               (uint32_t)(vc * W)) * sizeof(T)));
+                        const uint32_t po = need[x] ? (uint32_t)(((uint32_t)uu[x] * (uint32_t)k +
+                                                                   (uint32_t)(vc * W)) * sizeof(T))
+                                                    : 0xFFFFFFF0u;
+                        // skipped by the whole wave when no group changes user
+                        if (__builtin_amdgcn_ballot_w64(need[x]) != 0)
+                            p[x][v] = buf_ld<0, VT>(rp, po);
+                        else
+                            p[x][v] = (VT)(T)0;
+                    }
+                    if constexpr (KERN != MF_RBF) {
+                        bi[x] = buf_ld<0, T>(rbi, (uint32_t)ii[x] * (uint32_t)sizeof(T));
+                        bu[x] = buf_ld<0, T>(rbu, need[x] ? (uint32_t)uu[x] * (uint32_t)sizeof(T)
+                                                          : 0xFFFFFFF0u);
+                    } else {
+                        bi[x] = bu[x] = (T)0;
+                    }
+                }
+                // the user row of each rating: loaded, or carried from the
+                // previous rating of the run
+#pragma unroll
+                for (int x = 0; x < S; ++x) {
+#pragma unroll
+                    for (int v = 0; v < V; ++v) p[x][v] = need[x] ? p[x][v] : (x == 0 ? pp[v] : p[x - 1][v]);
+                    bu[x] = need[x] ? bu[x] : (x == 0 ? pbu : bu[x - 1]);
+                }
+#pragma unroll
+                for (int x = 0; x < S; ++x) {
+                    T part = (T)0;
+#pragma unroll
+                    for (int v = 0; v < V; ++v) {
+                        VT pv[1] = {p[x][v]}, qv[1] = {q[x][v]};
+                        const T pt = lane_partial<T, W, 1, KERN>(pv, qv);
+                        part += v * GS + l < kv ? pt : (T)0;
+                    }
+                    const T sm = group_sum<GS>(part);
+                    const T err = rr[x] - predict_one<T, KERN>(sm, bu[x], bi[x], h);   // :313
+                    if (hv[x] && l == 0) acc += (double)err * (double)err;
+                }
+#pragma unroll
+                for (int v = 0; v < V; ++v) pp[v] = p[S - 1][v];
+                pbu = bu[S - 1];
+                pu = uu[S - 1];
+            }
+        }
+    }
+    acc = wave_sum(acc);
+    __shared__ double red[kWavesPerBlock];
+    if (lane == 0) red[threadIdx.x / kWave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; ++w) t += red[w];
+        A.partials[blockIdx.x] = t;
+    }
+}
+
 __global__ void k_sum_partials(const double* part, int n, double* out);
 
 constexpr int kSseMaxBlocks = 2048;
@@ -549,6 +689,7 @@ struct SgdParams {
 struct SseParams {
     const int32_t* u; const int32_t* i; const void* r; int64_t n;
     double mu; const void* bu; const void* bi; const void* P; const void* Q;
+    int32_t n_users, n_items;
     int32_t k; int32_t kernel; double gamma, lo, hi;
     double* partials; double* sse_out; hipStream_t stream; SliceTab S;
 };
@@ -672,9 +813,43 @@ struct SseRun {
         a.Bu = static_cast<const T*>(p.bu); a.Bi = static_cast<const T*>(p.bi);
         a.n = p.n; a.k = p.k; a.bound = 0; a.out = nullptr; a.partials = p.partials;
         a.h = make_hyper<T>(p.mu, 0.0, 0.0, p.gamma, p.lo, p.hi);
-        const int blocks = (kSseMaxBlocks / p.S.n) * p.S.n;
-        hipLaunchKernelGGL((k_sse_stream<T, W, GS, V, KERN, S>), dim3(blocks), dim3(kBlock), 0,
-                           p.stream, a, p.S);
+        // One wave of workgroups: every resident slot gets one equal share of
+        // its slice (a second, partial round of workgroups would leave the
+        // chip part idle for a whole share).  MF_SSE_BLOCKS overrides (probes).
+        a.p_bytes = (uint64_t)p.n_users * p.k * sizeof(T);
+        a.q_bytes = (uint64_t)p.n_items * p.k * sizeof(T);
+        a.bu_bytes = (uint64_t)p.n_users * sizeof(T);
+        a.bi_bytes = (uint64_t)p.n_items * sizeof(T);
+        // k_sse_owned (default); MF_SSE_VARIANT=1 selects k_sse_stream (probes,
+        // tools/sse_probe.py) and so does a P or Q too large for a buffer
+        // resource.  Measured at C3 (rank 64, FP32): 2.49 vs 2.66 ms; the
+        // owned kernel without the wave-uniform skip of user-row loads took
+        // 2.72 ms, with non-temporal user streams 2.69 ms.
+        const char* ev = std::getenv("MF_SSE_VARIANT");
+        int var = ev && std::atoi(ev) == 1 ? 1 : 0;
+        if (a.p_bytes >= (1ull << 32) - 64 || a.q_bytes >= (1ull << 32) - 64) var = 1;  // buffer range
+        auto kfn = var == 1 ? k_sse_stream<T, W, GS, V, KERN, S>
+                            : k_sse_owned<T, W, GS, V, KERN, S>;
+        static int resident_tab[2] = {0, 0};     // per instantiation and variant
+        int& resident = resident_tab[var];
+        if (resident == 0) {
+            int dev = 0, cus = 0, per_cu = 0;
+            if (hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) ==
+                    hipSuccess &&
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kBlock, 0) ==
+                    hipSuccess && cus > 0 && per_cu > 0)
+                resident = cus * per_cu;
+            else
+                resident = kSseMaxBlocks;
+        }
+        int blocks = std::min(resident, kSseMaxBlocks);
+        if (const char* e = std::getenv("MF_SSE_BLOCKS")) {
+            const int v = std::atoi(e);
+            if (v > 0) blocks = std::min(v, kSseMaxBlocks);
+        }
+        blocks = std::max(p.S.n, (blocks / p.S.n) * p.S.n);
+        hipLaunchKernelGGL(kfn, dim3(blocks), dim3(kBlock), 0, p.stream, a, p.S);
         hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(kBlock), 0, p.stream,
                            (const double*)p.partials, blocks, p.sse_out);
         MF_HIP_CHECK(hipGetLastError());

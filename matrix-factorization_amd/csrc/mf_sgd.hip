@@ -1,6 +1,6 @@
 // mf_sgd.hip -- C ABI of the KernelMF hot path (include/mf_hip.h):
 //   mf_sgd_epoch  -> k_sgd_batch  (mf_rows.hpp; one launch per batch)
-//   mf_sse        -> k_sse_stream (mf_rows.hpp)
+//   mf_sse        -> k_sse_owned (mf_rows.hpp)
 //   mf_predict    -> k_read       (this file)
 //
 // Compiled with -ffp-contract=off: every scalar expression rounds like the
@@ -348,12 +348,12 @@ extern "C" int mf_sse(const int32_t* user_ids, const int32_t* item_ids,
                       const void* ratings, int64_t n_ratings,
                       double global_mean, const void* user_biases,
                       const void* item_biases, const void* user_features,
-                      const void* item_features, int32_t n_factors,
-                      int32_t kernel, int32_t dtype, double gamma,
+                      const void* item_features, int32_t n_users, int32_t n_items,
+                      int32_t n_factors, int32_t kernel, int32_t dtype, double gamma,
                       double min_rating, double max_rating,
                       const int64_t* slice_offsets, int32_t n_slices, void* workspace,
                       double* sse_out, void* stream) {
-    if (n_ratings < 0 || !sse_out || !workspace ||
+    if (n_ratings < 0 || !sse_out || !workspace || n_users < 0 || n_items < 0 ||
         (slice_offsets && (n_slices < 1 || n_slices > kMaxSlices))) {
         set_error("mf_sse: bad arguments (n_slices must be in [1, %d])", kMaxSlices);
         return MF_ERR_INVALID;
@@ -376,8 +376,9 @@ extern "C" int mf_sse(const int32_t* user_ids, const int32_t* item_ids,
         return MF_OK;
     }
     SseParams P{user_ids, item_ids, ratings, n_ratings, global_mean, user_biases,
-                item_biases, user_features, item_features, n_factors, kernel, gamma,
-                min_rating, max_rating, (double*)workspace, sse_out, (hipStream_t)stream, S};
+                item_biases, user_features, item_features, n_users, n_items, n_factors,
+                kernel, gamma, min_rating, max_rating, (double*)workspace, sse_out,
+                (hipStream_t)stream, S};
     if (dtype == MF_F32) return sse_launch_f32(P);
     if (dtype == MF_F64) return sse_launch_f64(P);
     set_error("unknown dtype code %d", dtype);

@@ -531,7 +531,8 @@ class SGDEngine:
                 offs = self.eval_offs
                 _lib.call("mf_sse", _tp(self.eu), _tp(self.ei), _tp(self.er), self.n,
                           self.global_mean, _tp(self.bu), _tp(self.bi), _tp(self.P),
-                          _tp(self.Q), self.k, self.kcode, self.dcode, self.gamma,
+                          _tp(self.Q), self.n_users, self.n_items, self.k, self.kcode,
+                          self.dcode, self.gamma,
                           self.min_rating, self.max_rating, _np(offs),
                           0 if offs is None else len(offs) - 1, _tp(self.ws), out,
                           self.stream)
