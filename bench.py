@@ -59,6 +59,14 @@ WORKLOADS = {
            "synthetic 1Mx100K 100M-nnz rank-128 ALS (MFMA Gramian)"),
     "c5_small": (100_000, 10_000, 5_000_000, 128, "als",
                  "synthetic 100Kx10K 5M-nnz rank-128 ALS (smoke)"),
+    # probes (not bench lines): one rank's share of C3 at N = 2 / 4 / 8
+    # (users sharded), to see the per-GPU epoch of the strong-scaling runs
+    "c3_shard2": (500_000, 100_000, 50_000_000, 64, "linear",
+                  "probe: C3 user shard at N=2 (500Kx100K 50M-nnz rank-64 linear SGD)"),
+    "c3_shard4": (250_000, 100_000, 25_000_000, 64, "linear",
+                  "probe: C3 user shard at N=4 (250Kx100K 25M-nnz rank-64 linear SGD)"),
+    "c3_shard8": (125_000, 100_000, 12_500_000, 64, "linear",
+                  "probe: C3 user shard at N=8 (125Kx100K 12.5M-nnz rank-64 linear SGD)"),
     # probes (not bench lines): P that fits the 256 MiB Infinity Cache
     "c3_u250k": (250_000, 100_000, 100_000_000, 64, "linear",
                  "probe: synthetic 250Kx100K 100M-nnz rank-64 linear SGD"),
