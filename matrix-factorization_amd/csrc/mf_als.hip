@@ -386,21 +386,41 @@ __global__ __launch_bounds__(kAlsThreads, 2) void k_als_solve(AlsArgs A) {
     const float b = (g - num) / (((float)cnt + A.reg) - den);
     const float w0 = (f0 - b * s0) * i0, w1 = (f1 - b * s1) * i1;
     float acc0 = 0.f, acc1 = 0.f, x0 = 0.f, x1 = 0.f;
-    float c0n = v0 ? M[a0 * LD + (KP - 1)] : 0.f, c1n = v1 ? M[a1 * LD + (KP - 1)] : 0.f;
-    for (int j = KP - 1; j >= 0; --j) {
-        const float c0 = c0n, c1 = c1n;           // column j of rows a0, a1
-        if (j > 0) {                              // prefetch column j - 1
-            c0n = v0 ? M[a0 * LD + j - 1] : 0.f;
-            c1n = v1 ? M[a1 * LD + j - 1] : 0.f;
+    // Columns j of rows a0, a1 come from LDS in blocks of 8, one block ahead
+    // (a load one column ahead left most of the LDS latency on the critical
+    // path of the readlane chain); two register blocks used alternately.
+    constexpr int BJ = 8;
+    static_assert(KP % (2 * BJ) == 0, "back substitution blocks");
+    float cA0[BJ], cA1[BJ], cB0[BJ], cB1[BJ];
+    auto load_cols = [&](int jb, float (&c0)[BJ], float (&c1)[BJ]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < BJ; ++u) {
+            c0[u] = v0 ? M[a0 * LD + jb + u] : 0.f;
+            c1[u] = v1 ? M[a1 * LD + jb + u] : 0.f;
         }
-        const float cand = j >= kWave ? (w1 - acc1) : (w0 - acc0);
-        const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand), j & (kWave - 1)));
-        if (lane == (j & (kWave - 1))) {
-            if (j >= kWave) x1 = xj;
-            else x0 = xj;
+    };
+    auto solve_cols = [&](int jb, const float (&c0)[BJ], const float (&c1)[BJ])
+                          __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = BJ - 1; u >= 0; --u) {
+            const int j = jb + u;
+            const float cand = j >= kWave ? (w1 - acc1) : (w0 - acc0);
+            const float xj =
+                __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand), j & (kWave - 1)));
+            if (lane == (j & (kWave - 1))) {
+                if (j >= kWave) x1 = xj;
+                else x0 = xj;
+            }
+            if (v0 && a0 < j) acc0 = acc0 + (c0[u] * i0) * xj;
+            if (v1 && a1 < j) acc1 = acc1 + (c1[u] * i1) * xj;
         }
-        if (v0 && a0 < j) acc0 = acc0 + (c0 * i0) * xj;
-        if (v1 && a1 < j) acc1 = acc1 + (c1 * i1) * xj;
+    };
+    load_cols(KP - BJ, cA0, cA1);
+    for (int jb = KP - BJ; jb >= 0; jb -= 2 * BJ) {
+        load_cols(jb - BJ, cB0, cB1);             // jb - BJ >= 0: KP % (2 BJ) == 0
+        solve_cols(jb, cA0, cA1);
+        if (jb - 2 * BJ >= 0) load_cols(jb - 2 * BJ, cA0, cA1);
+        solve_cols(jb - BJ, cB0, cB1);
     }
     float* out = A.feat + (int64_t)e * k;
     if (v0 && a0 < k) out[a0] = x0;

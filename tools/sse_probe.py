@@ -21,6 +21,8 @@ from matrix_factorization.engine import SGDEngine
 def main():
     runs = [tuple(int(y) for y in x.split(":")) for x in sys.argv[1:]] or [(0, 0)]
     nu, ni, nnz, k = 1_000_000, 100_000, 100_000_000, 64
+    import matrix_factorization.engine as E
+    E.N_SLICES = int(os.environ.get("SSE_PROBE_SLICES", E.N_SLICES))   # evaluation slices
     u, i, r = bench.synth(nu, ni, nnz)
     eng = SGDEngine(u, i, r, nu, ni, k, "linear", "float32", "cuda:0",
                     global_mean=float(r.mean()), min_rating=1, max_rating=5)
@@ -49,7 +51,7 @@ def main():
         ms = t0.elapsed_time(t1) / reps
         sse = eng.sse_values(1)[0]
         ref = sse if ref is None else ref
-        print(f"variant={var} blocks={g or 'default'} sse_ms={ms:.3f} sse={sse:.6f} "
+        print(f"slices={E.N_SLICES} variant={var} blocks={g or 'default'} sse_ms={ms:.3f} sse={sse:.6f} "
               f"rel_to_first={abs(sse - ref) / ref:.2e}", flush=True)
 
 
