@@ -250,6 +250,8 @@ def main() -> int:
                     help="ratings in the CPU-oracle sample (0 = skip the CPU leg)")
     ap.add_argument("--no-phase-timing", action="store_true",
                     help="do not bracket the SGD / RMSE phases with hipEvents")
+    ap.add_argument("--blocks", type=int, default=None,
+                    help="strata: B (probes; default: engine.choose_strata_blocks)")
     ap.add_argument("--schedule", default="strata", choices=["strata", "colored"],
                     help="strata: B x B blocks, item slabs in LDS (mf_strata.hpp); "
                          "colored: one launch per edge colour (mf_rows.hpp)")
@@ -304,7 +306,7 @@ def main() -> int:
     t0 = time.time()
     strata = args.schedule == "strata"
     if strata:
-        plan = eng.prepare_strata()
+        plan = eng.prepare_strata(n_blocks=args.blocks)
         nb = plan.B
         strat_sizes = plan.stratum_sizes()           # ratings per stratum (launch)
         fill = n_local / max(plan.n_positions, 1)

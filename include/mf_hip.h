@@ -168,6 +168,11 @@ int mf_strata_status(const void* workspace, int32_t n_blocks, void* stream);
 size_t mf_strata_lds_bytes(int32_t max_block_items, int32_t max_block_users,
                            int32_t n_factors, int32_t dtype);
 int32_t mf_strata_lds_limit(void);
+/* Diagnostic (tools/strata_probe.py): when `probe` (DEVICE, 4 * n_seq * B
+ * int64) is set, the persistent strata kernel records s_memrealtime stamps
+ * (100 MHz) per (position t, workgroup w) at [(t*B + w)*4 + q]: q = 0 wait
+ * start, 1 wait end, 2 block end, 3 signal.  NULL turns it off (default). */
+int mf_strata_set_probe(int64_t* probe);
 /* Rating slots per step of the strata kernel for (n_factors, dtype); -1 on
  * invalid arguments. */
 int32_t mf_strata_slots(int32_t n_factors, int32_t dtype);

@@ -252,6 +252,16 @@ extern "C" size_t mf_strata_lds_bytes(int32_t max_block_items, int32_t max_block
 
 extern "C" int32_t mf_strata_lds_limit(void) { return kLdsLimit; }
 
+namespace mf {
+static int64_t* g_strata_probe = nullptr;
+int64_t* strata_probe_ptr() { return g_strata_probe; }
+}  // namespace mf
+
+extern "C" int mf_strata_set_probe(int64_t* probe) {
+    mf::g_strata_probe = probe;
+    return MF_OK;
+}
+
 extern "C" size_t mf_strata_workspace_bytes(int32_t n_blocks, int32_t n_seq) {
     return n_blocks > 0 && n_seq >= 0 ? strata_ws_bytes(n_blocks, n_seq) : 0;
 }

@@ -71,6 +71,7 @@ struct StrataArgs {
     int32_t upd_item;
     uint64_t p_bytes;        // bytes of P (write-through buffer stores: < 4 GiB)
     Hyper<T> h;
+    int64_t* probe;          // nullable: persistent-kernel phase stamps (mf_strata_set_probe)
 };
 
 // first step of block `blk` in this epoch (mirrored by engine.strata_mix)
@@ -351,10 +352,17 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<
     T* Bus = Bis + nqi;
     const Hyper<T> h = hyper_regs(A.h);
     strata_stage_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
+    // probe: s_memrealtime (100 MHz) at wait start / wait end / block end /
+    // signal, 4 stamps per (position t, workgroup w)
+    auto stamp = [&](int t, int q) __attribute__((always_inline)) {
+        if (A.probe && threadIdx.x == 0)
+            A.probe[((int64_t)t * B + w) * 4 + q] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    };
     for (int t = 0; t < n_seq; ++t) {
         const int s = seq[t];
         const int ub = (w + s) % B;
         const int ulo = A.ubnd[ub], nus = A.ubnd[ub + 1] - ulo;
+        stamp(t, 0);
         if (threadIdx.x == 0) {
             int ab = 0;
             if (t > 0) {
@@ -377,6 +385,7 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<
         }
         __syncthreads();
         if (s_abort) return;
+        stamp(t, 1);
         if constexpr (KERN != MF_RBF)
             for (int x = threadIdx.x; x < nus; x += kStrataThreads)
                 Bus[x] = __hip_atomic_load(A.Bu + ulo + x, __ATOMIC_RELAXED,
@@ -385,6 +394,7 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<
         strata_block<T, W, GS, V, KERN, S, true>(A, (int64_t)s * B + w, ulo, ilo, Qs, Bis, Bus,
                                                  h);
         __syncthreads();
+        stamp(t, 2);
         if constexpr (KERN != MF_RBF) {
             if (A.upd_user)
                 for (int x = threadIdx.x; x < nus; x += kStrataThreads)
@@ -397,10 +407,15 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<
         __syncthreads();
         if (threadIdx.x == 0)
             __hip_atomic_store(done + w, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        stamp(t, 3);
     }
     __syncthreads();
     strata_store_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
 }
+
+// diagnostic: device buffer for the persistent kernel's phase stamps
+// (mf_strata_set_probe; 4 * n_seq * B int64), nullptr = off
+int64_t* strata_probe_ptr();
 
 struct StrataParams {
     const int32_t* u; const int32_t* i; const void* r;
@@ -474,6 +489,7 @@ struct StrataRun {
         a.B = p.B; a.seed = p.seed; a.k = p.k; a.upd_user = p.uu; a.upd_item = p.ui;
         a.p_bytes = (uint64_t)p.n_users * (uint64_t)p.k * sizeof(T);
         a.h = make_hyper<T>(p.mu, p.lr, p.reg, p.gamma, p.lo, p.hi);
+        a.probe = strata_probe_ptr();
         hipEvent_t ev[2] = {nullptr, nullptr};
         if (p.kernel_ms) {
             MF_HIP_CHECK(hipEventCreate(&ev[0]));

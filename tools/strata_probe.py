@@ -1,0 +1,74 @@
+#!/usr/bin/env python
+"""Phase stamps of the persistent strata kernel (mf_strata_set_probe):
+per (position t, workgroup w) the wait for the user range, the block's
+steps, the hand-off signal; mean and spread over one epoch.
+Usage: python tools/strata_probe.py [--workload c2] [--blocks B]"""
+import argparse
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "matrix-factorization_amd"))
+
+import numpy as np
+import torch
+
+import bench
+from matrix_factorization import _lib
+from matrix_factorization.engine import SGDEngine
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="c2")
+    ap.add_argument("--blocks", type=int, default=None)
+    args = ap.parse_args()
+    nu, ni, nnz, k, kernel, _ = bench.WORKLOADS[args.workload]
+    u, i, r = bench.synth(nu, ni, nnz)
+    eng = SGDEngine(u, i, r, nu, ni, k, kernel, "float32", "cuda:0", gamma=1.0 / k,
+                    min_rating=1, max_rating=5, global_mean=float(r.mean()))
+    plan = eng.prepare_strata(n_blocks=args.blocks)
+    B = plan.B
+    rs = np.random.RandomState(0)
+    eng.load_params(rs.normal(0, 0.1, (nu, k)).astype(np.float32),
+                    rs.normal(0, 0.1, (ni, k)).astype(np.float32),
+                    np.zeros(nu, np.float32), np.zeros(ni, np.float32))
+    for ep in range(2):
+        eng.epoch_strata(rs.permutation(B).astype(np.int32), ep, 0.01, 0.02)
+    torch.cuda.synchronize()
+    probe = torch.zeros(4 * B * B, dtype=torch.int64, device="cuda:0")
+    _lib.call("mf_strata_set_probe", ctypes.c_void_p(probe.data_ptr()))
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    t0.record()
+    eng.epoch_strata(rs.permutation(B).astype(np.int32), 7, 0.01, 0.02)
+    t1.record()
+    torch.cuda.synchronize()
+    _lib.call("mf_strata_set_probe", None)
+    eng.check_strata()
+    st = probe.cpu().numpy().reshape(B, B, 4).astype(np.float64) * 10.0 / 1000.0   # us
+    if not np.all(st[:, :, 3] > 0):
+        print("probe incomplete (per-stratum fallback ran?)")
+        return
+    wait = st[:, :, 1] - st[:, :, 0]
+    block = st[:, :, 2] - st[:, :, 1]
+    sig = st[:, :, 3] - st[:, :, 2]
+    gap = st[1:, :, 0] - st[:-1, :, 3]
+    span = st[:, :, 3].max() - st[:, :, 0].min()
+    steps = np.diff(plan.bstep).reshape(B, B)            # [s, w]
+    print(f"{args.workload}: B={B} NS={plan.NS} epoch kernel {t0.elapsed_time(t1):.3f} ms, "
+          f"stamp span {span / 1e3:.3f} ms, per position {span / B:.2f} us")
+    for name, a in (("wait", wait), ("block", block), ("signal", sig), ("gap", gap)):
+        print(f"  {name:6s} mean {a.mean():7.2f} us  p50 {np.median(a):7.2f}  p90 "
+              f"{np.percentile(a, 90):7.2f}  max {a.max():7.2f}")
+    print(f"  steps per block: mean {steps.mean():.2f} max {steps.max()}; "
+          f"block us per step {block.sum() / max(steps.sum(), 1):.2f}")
+    busy = (block + sig).sum(axis=0)                      # per workgroup
+    print(f"  per-workgroup busy (block+signal) mean {busy.mean() / 1e3:.3f} ms, "
+          f"wait total mean {wait.sum(axis=0).mean() / 1e3:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()
