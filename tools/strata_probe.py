@@ -66,8 +66,16 @@ def main():
     print(f"  steps per block: mean {steps.mean():.2f} max {steps.max()}; "
           f"block us per step {block.sum() / max(steps.sum(), 1):.2f}")
     busy = (block + sig).sum(axis=0)                      # per workgroup
-    print(f"  per-workgroup busy (block+signal) mean {busy.mean() / 1e3:.3f} ms, "
+    print(f"  per-workgroup busy (block+signal) mean {busy.mean() / 1e3:.3f} ms "
+          f"(min {busy.min() / 1e3:.3f}, max {busy.max() / 1e3:.3f}), "
           f"wait total mean {wait.sum(axis=0).mean() / 1e3:.3f} ms")
+    xcd = np.array([busy[w::8].mean() for w in range(min(8, B))]) / 1e3
+    print("  busy by XCD (w % 8), ms: " + " ".join(f"{x:.3f}" for x in xcd))
+    bt = block.T                                          # [w, t]
+    rel = bt / bt.mean(axis=1, keepdims=True)
+    print(f"  block time / its workgroup's mean: p10 {np.percentile(rel, 10):.2f} "
+          f"p90 {np.percentile(rel, 90):.2f}; workgroup means p10 "
+          f"{np.percentile(bt.mean(axis=1), 10):.1f} p90 {np.percentile(bt.mean(axis=1), 90):.1f} us")
 
 
 if __name__ == "__main__":
