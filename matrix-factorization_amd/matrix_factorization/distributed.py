@@ -92,12 +92,25 @@ class ReplicaExchange:
 
 def sharded_epochs(engine: SGDEngine, exchange: Optional[ReplicaExchange], n_epochs: int,
                    lr: float, reg: float, seed: int, first_epoch: int = 0,
-                   timing: bool = False) -> list:
-    """Run colored epochs on this rank; returns per-epoch summed SGD kernel ms
-    (timing) -- the SSE of epoch j lands in engine.sse_buf[first_epoch + j]."""
-    if engine.colored is None:
-        engine.prepare_colored()
-    nb = len(engine.colored) - 1
+                   timing: bool = False, schedule: str = "colored",
+                   n_blocks: Optional[int] = None) -> list:
+    """Run ``schedule`` ("colored" or "strata") epochs on this rank; returns
+    per-epoch SGD kernel timings (timing) -- the SSE of epoch j lands in
+    engine.sse_buf[first_epoch + j].  Epoch ep draws its colour / stratum
+    order (and, for strata, the step rotation) from RandomState(seed, ep), so
+    every rank's draws are reproducible on their own.  ``n_blocks``: strata
+    B for this rank's plan (default: engine.choose_strata_blocks)."""
+    strata = schedule == "strata"
+    if schedule not in ("colored", "strata"):
+        raise ValueError(f"schedule must be 'colored' or 'strata', got {schedule!r}")
+    if strata:
+        if engine.strata is None:
+            engine.prepare_strata(n_blocks=n_blocks)
+        nb = engine.strata.B
+    else:
+        if engine.colored is None:
+            engine.prepare_colored()
+        nb = len(engine.colored) - 1
     kms = []
     for j in range(n_epochs):
         ep = first_epoch + j
@@ -105,11 +118,17 @@ def sharded_epochs(engine: SGDEngine, exchange: Optional[ReplicaExchange], n_epo
         seq = rs_ep.permutation(nb).astype(np.int32)
         if exchange is not None:
             exchange.begin_epoch()
-        ms = engine.epoch_colored(seq, lr, reg, timing=timing)
+        if strata:
+            rot = int(rs_ep.randint(0, 2**31 - 1))
+            ms = engine.epoch_strata(seq, rot, lr, reg, timing=timing)
+        else:
+            ms = engine.epoch_colored(seq, lr, reg, timing=timing)
         if exchange is not None:
             exchange.end_epoch()
         engine.sse_async(ep)
         kms.append(ms)
+    if strata:
+        engine.check_strata()
     return kms
 
 

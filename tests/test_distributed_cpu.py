@@ -21,6 +21,7 @@ import oracle
 
 NU, NI, NNZ, K = 300, 80, 6000, 8
 LR, REG, EPOCHS, SEED = 0.02, 0.05, 3, 99
+STRATA_B = 3                                     # strata per epoch on each rank
 
 
 def _data():
@@ -35,13 +36,16 @@ def _data():
 
 
 class CpuEngine:
-    """Test double of SGDEngine for the colored schedule (oracle sweeps)."""
+    """Test double of SGDEngine for the colored and strata schedules (oracle
+    sweeps in the schedule's serial order; the plans are the product's)."""
 
     def __init__(self, u, i, r, n_users, n_items, k, mu):
         self.u_host, self.i_host, self.r_host = u, i, r
         self.n, self.n_users, self.n_items, self.k = len(u), n_users, n_items, k
         self.global_mean = mu
         self.colored = None
+        self.strata = None
+        self.dcode = 1                           # MF_F64
         self.sse_buf = torch.zeros(16, dtype=torch.float64)
         self.tdt, self.dev = torch.float64, torch.device("cpu")
         self.P = self.Q = self.bu = self.bi = None
@@ -65,6 +69,28 @@ class CpuEngine:
                                                  self.r_host[sched])
         self.colored = offs
         return len(offs) - 1
+
+    def prepare_strata(self, n_blocks=None):
+        from matrix_factorization.engine import (StrataPlan, balanced_bounds, sched_strata,
+                                                 strata_slots)
+
+        B = STRATA_B if n_blocks is None else n_blocks
+        ub = balanced_bounds(self.u_host, self.n_users, B)
+        ib = balanced_bounds(self.i_host, self.n_items, B)
+        ns = strata_slots(self.k, self.dcode)
+        sched, bstep = sched_strata(self.u_host, self.i_host, self.n_users, self.n_items, B,
+                                    ub, ib, ns)
+        self.strata = StrataPlan(B, ns, ub, ib, bstep, sched)
+        return self.strata
+
+    def epoch_strata(self, seq, seed, lr, reg, timing=False):
+        order = self.strata.serial_order(seq, seed)
+        oracle.sgd_pass(self.u_host, self.i_host, self.r_host, self.global_mean,
+                        self.bu.numpy(), self.bi.numpy(), self.P.numpy(), self.Q.numpy(),
+                        lr=lr, reg=reg, order=order)
+
+    def check_strata(self):
+        pass
 
     def epoch_colored(self, seq, lr, reg, timing=False):
         order = np.concatenate([np.arange(self.colored[b], self.colored[b + 1])
@@ -94,7 +120,7 @@ def _exchange_cls():
     return CpuExchange
 
 
-def _run_rank(rank, world, port, out_dir):
+def _run_rank(rank, world, port, out_dir, schedule="colored"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -110,7 +136,7 @@ def _run_rank(rank, world, port, out_dir):
     eng.load_params(P=P0[lo:hi], bu=np.zeros(hi - lo))
     ex = _exchange_cls()(eng)
     ex.bind(Q0, np.zeros(NI))
-    sharded_epochs(eng, ex, EPOCHS, LR, REG, SEED)
+    sharded_epochs(eng, ex, EPOCHS, LR, REG, SEED, schedule=schedule, n_blocks=STRATA_B)
     rm = global_rmse(eng, EPOCHS, NNZ)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), Q=eng.Q.numpy(), bi=eng.bi.numpy(),
              P=eng.P.numpy(), bu=eng.bu.numpy(), lo=lo, hi=hi, rmse=np.array(rm))
@@ -125,7 +151,7 @@ def _free_port():
     return port
 
 
-def _simulate(world):
+def _simulate(world, schedule="colored"):
     """Single-process restatement of the same algorithm."""
     from matrix_factorization.distributed import local_shard, shard_users
 
@@ -138,7 +164,10 @@ def _simulate(world):
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         e = CpuEngine(lu, li, lr_, hi - lo, NI, K, mu)
         e.load_params(P=P0[lo:hi], bu=np.zeros(hi - lo), Q=Q0, bi=np.zeros(NI))
-        e.prepare_colored()
+        if schedule == "strata":
+            e.prepare_strata(STRATA_B)
+        else:
+            e.prepare_colored()
         engs.append(e)
     Q = Q0.copy()
     bi = np.zeros(NI)
@@ -149,9 +178,13 @@ def _simulate(world):
         for e in engs:
             e.Q = torch.as_tensor(Q.copy())
             e.bi = torch.as_tensor(bi.copy())
-            nb = len(e.colored) - 1
-            seq = np.random.RandomState((SEED * 1000003 + ep) & 0x7FFFFFFF).permutation(nb)
-            e.epoch_colored(seq, LR, REG)
+            rs_ep = np.random.RandomState((SEED * 1000003 + ep) & 0x7FFFFFFF)
+            if schedule == "strata":
+                seq = rs_ep.permutation(e.strata.B)
+                e.epoch_strata(seq, int(rs_ep.randint(0, 2**31 - 1)), LR, REG)
+            else:
+                seq = rs_ep.permutation(len(e.colored) - 1)
+                e.epoch_colored(seq, LR, REG)
             dQ += e.Q.numpy() - Q
             dbi += e.bi.numpy() - bi
         Q = Q + dQ
@@ -177,15 +210,16 @@ def test_shard_users_balances_ratings():
 
 
 @pytest.mark.timeout(300)
-def test_two_rank_gloo_exchange_matches_simulation(tmp_path):
+@pytest.mark.parametrize("schedule", ["colored", "strata"])
+def test_two_rank_gloo_exchange_matches_simulation(tmp_path, schedule):
     world = 2
-    mp.start_processes(_run_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_run_rank, args=(world, _free_port(), str(tmp_path), schedule),
+                       nprocs=world, join=True, start_method="spawn")
     res = [dict(np.load(tmp_path / f"rank{k}.npz")) for k in range(world)]
     # every rank ends with the same item replica
     assert np.array_equal(res[0]["Q"], res[1]["Q"])
     assert np.array_equal(res[0]["bi"], res[1]["bi"])
-    Q, bi, rmse, engs, bounds = _simulate(world)
+    Q, bi, rmse, engs, bounds = _simulate(world, schedule)
     assert np.max(np.abs(res[0]["Q"] - Q)) < 1e-12
     assert np.max(np.abs(res[0]["bi"] - bi)) < 1e-12
     for k in range(world):

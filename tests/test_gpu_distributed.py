@@ -14,7 +14,7 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 
-def _rank(rank, world, port, out):
+def _rank(rank, world, port, out, schedule="colored"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch
@@ -23,7 +23,7 @@ def _rank(rank, world, port, out):
     from matrix_factorization.distributed import (ReplicaExchange, global_rmse, local_shard,
                                                   shard_users, sharded_epochs)
     from matrix_factorization.engine import SGDEngine
-    from test_distributed_cpu import EPOCHS, K, LR, NI, NNZ, NU, REG, SEED, _data
+    from test_distributed_cpu import EPOCHS, K, LR, NI, NNZ, NU, REG, SEED, STRATA_B, _data
 
     u, i, r, P0, Q0 = _data()
     mu = float(r.mean())
@@ -35,7 +35,7 @@ def _rank(rank, world, port, out):
     eng.load_params(P=P0[lo:hi], bu=np.zeros(hi - lo))
     ex = ReplicaExchange(eng)
     ex.bind(Q0, np.zeros(NI))
-    sharded_epochs(eng, ex, EPOCHS, LR, REG, SEED)
+    sharded_epochs(eng, ex, EPOCHS, LR, REG, SEED, schedule=schedule, n_blocks=STRATA_B)
     rm = global_rmse(eng, EPOCHS, NNZ)
     P, Q, bu, bi = eng.params_numpy()
     np.savez(os.path.join(out, f"g{rank}.npz"), P=P, Q=Q, bi=bi, rmse=np.array(rm))
@@ -43,15 +43,18 @@ def _rank(rank, world, port, out):
 
 
 @pytest.mark.timeout(600)
-def test_two_ranks_on_one_gpu_match_cpu_simulation(tmp_path):
+@pytest.mark.parametrize("schedule", ["colored", "strata"])
+def test_two_ranks_on_one_gpu_match_cpu_simulation(tmp_path, schedule):
+    """strata: both ranks' persistent kernels (3 workgroups each) share the
+    card; the result is the serial-order simulation's."""
     from test_distributed_cpu import _free_port, _simulate
 
     world = 2
-    mp.start_processes(_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_rank, args=(world, _free_port(), str(tmp_path), schedule),
+                       nprocs=world, join=True, start_method="spawn")
     res = [dict(np.load(tmp_path / f"g{k}.npz")) for k in range(world)]
     assert np.array_equal(res[0]["Q"], res[1]["Q"])
-    Q, bi, rmse, engs, bounds = _simulate(world)
+    Q, bi, rmse, engs, bounds = _simulate(world, schedule)
     assert np.max(np.abs(res[0]["Q"] - Q)) < 1e-10
     assert np.max(np.abs(res[0]["bi"] - bi)) < 1e-10
     for k in range(world):
