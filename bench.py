@@ -255,6 +255,9 @@ def main() -> int:
     ap.add_argument("--schedule", default="strata", choices=["strata", "colored"],
                     help="strata: B x B blocks, item slabs in LDS (mf_strata.hpp); "
                          "colored: one launch per edge colour (mf_rows.hpp)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 process group: nccl (= RCCL, one GPU per rank) or gloo "
+                         "(rehearsal: ranks may share a GPU, LOCAL_RANK mod device count)")
     args = ap.parse_args()
 
     import torch
@@ -270,10 +273,16 @@ def main() -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
-    dev = torch.device("cuda", local_rank)
+    if args.backend == "gloo":
+        dev = torch.device("cuda", local_rank % max(torch.cuda.device_count(), 1))
+    else:
+        dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     _lib.load()
 
     nu, ni, nnz, k, kernel, desc = WORKLOADS[args.workload]

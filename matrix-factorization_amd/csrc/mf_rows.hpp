@@ -830,7 +830,15 @@ struct SseRun {
         if (a.p_bytes >= (1ull << 32) - 64 || a.q_bytes >= (1ull << 32) - 64) var = 1;  // buffer range
         auto kfn = var == 1 ? k_sse_stream<T, W, GS, V, KERN, S>
                             : k_sse_owned<T, W, GS, V, KERN, S>;
-        static int resident_tab[2] = {0, 0};     // per instantiation and variant
+        // FP32 rows of one vector per lane (rank 64): a whole chunk of 16
+        // ratings per group per step (C3: 2.45 vs 2.52 ms with S = 4, 2.46
+        // with 8; tools/sse_probe.py).  Probes: 2 = 8 per step, 3 = SlotsFor.
+        if constexpr (GS == 16 && V == 1 && std::is_same<T, float>::value) {
+            if (var == 0) kfn = k_sse_owned<T, W, GS, V, KERN, 16>;
+            if (var == 0 && ev && std::atoi(ev) == 2) { var = 2; kfn = k_sse_owned<T, W, GS, V, KERN, 8>; }
+            if (var == 0 && ev && std::atoi(ev) == 3) { var = 3; kfn = k_sse_owned<T, W, GS, V, KERN, S>; }
+        }
+        static int resident_tab[4] = {0, 0, 0, 0};   // per instantiation and variant
         int& resident = resident_tab[var];
         if (resident == 0) {
             int dev = 0, cus = 0, per_cu = 0;
