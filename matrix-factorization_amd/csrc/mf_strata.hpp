@@ -104,9 +104,13 @@ __device__ __forceinline__ void lds_barrier() {
 // WT: user rows are loaded and stored with sc1 buffer ops (write-through
 // stores, L1-bypassing loads), the hand-off form of the persistent kernel: no
 // L2 write-back fence on the producer, no L1 invalidate on the consumer.
-template <typename T, int W, int GS, int V, int KERN, int S, bool WT = false>
+// BUS_IN: the block stages its user-bias slice itself (handed-off bytes, sc1
+// loads), issued behind the pipeline prologue's loads so the two global-load
+// latencies at the start of a block overlap (nus: users in the range).
+template <typename T, int W, int GS, int V, int KERN, int S, bool WT = false, bool BUS_IN = false>
 __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk, int ulo, int ilo,
-                                             T* Qs, T* Bis, T* Bus, const Hyper<T> h) {
+                                             T* Qs, T* Bis, T* Bus, const Hyper<T> h,
+                                             int nus = 0) {
     using VT = typename VecOf<T, W>::type;
     constexpr int R = kWave / GS;
     constexpr int RPW = S * R;
@@ -242,6 +246,26 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
         load_tri(0, ta);
         load_tri(1, tb);
         unpack_gather(ta, ra);
+    }
+    if constexpr (BUS_IN && KERN != MF_RBF) {
+        // all loads issued before the first LDS write waits for them
+        constexpr int kBu = 4;
+        T bt[kBu];
+        const int last = nus > 0 ? nus - 1 : 0;
+#pragma unroll
+        for (int c = 0; c < kBu; ++c) {
+            const int x = (int)threadIdx.x + c * kStrataThreads;
+            bt[c] = __hip_atomic_load(A.Bu + ulo + (x < last ? x : last), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);            // sc1 load
+        }
+#pragma unroll
+        for (int c = 0; c < kBu; ++c) {
+            const int x = (int)threadIdx.x + c * kStrataThreads;
+            if (x < nus) Bus[x] = bt[c];
+        }
+        for (int x = (int)threadIdx.x + kBu * kStrataThreads; x < nus; x += kStrataThreads)
+            Bus[x] = __hip_atomic_load(A.Bu + ulo + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lds_barrier();
     }
     for (int t = 0; t < nst; t += 2) {
         step(t, ta, tb, ra, rb);
@@ -386,13 +410,9 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<
         __syncthreads();
         if (s_abort) return;
         stamp(t, 1);
-        if constexpr (KERN != MF_RBF)
-            for (int x = threadIdx.x; x < nus; x += kStrataThreads)
-                Bus[x] = __hip_atomic_load(A.Bu + ulo + x, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);          // sc1 load
-        __syncthreads();
-        strata_block<T, W, GS, V, KERN, S, true>(A, (int64_t)s * B + w, ulo, ilo, Qs, Bis, Bus,
-                                                 h);
+        // the user-bias slice is staged inside the block, behind its prologue
+        strata_block<T, W, GS, V, KERN, S, true, true>(A, (int64_t)s * B + w, ulo, ilo, Qs, Bis,
+                                                       Bus, h, nus);
         __syncthreads();
         stamp(t, 2);
         if constexpr (KERN != MF_RBF) {
