@@ -56,10 +56,12 @@ enum {
     MF_FLAG_NT_ITEM = 4,      /* (unused by the current kernels)                */
     MF_FLAG_XCD_CLAIM = 8,    /* workgroups claim the tiles of the item slice of
                                  the XCD they run on (needs `workspace`)        */
-    MF_FLAG_PERSISTENT = 16   /* mf_sgd_epoch_strata: the whole epoch in one
+    MF_FLAG_PERSISTENT = 16,  /* mf_sgd_epoch_strata: the whole epoch in one
                                  launch, item slabs resident in LDS (needs
                                  `workspace`; falls back to one launch per
                                  stratum when the grid cannot be co-resident) */
+    MF_FLAG_DEEP_PIPE = 32    /* with MF_FLAG_PERSISTENT: user rows gathered two
+                                 steps ahead (blocks of few steps)               */
 };
 
 const char* mf_last_error(void);

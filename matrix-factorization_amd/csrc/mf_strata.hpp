@@ -107,7 +107,12 @@ __device__ __forceinline__ void lds_barrier() {
 // BUS_IN: the block stages its user-bias slice itself (handed-off bytes, sc1
 // loads), issued behind the pipeline prologue's loads so the two global-load
 // latencies at the start of a block overlap (nus: users in the range).
-template <typename T, int W, int GS, int V, int KERN, int S, bool WT = false, bool BUS_IN = false>
+// DEPTH: user rows gathered DEPTH steps ahead (1: rows of t+1 and triples of
+// t+2 in flight while step t applies; 2: rows of t+1 and t+2, triples of t+3
+// and t+4 -- for blocks of few steps, where each step otherwise waits one
+// load latency).
+template <typename T, int W, int GS, int V, int KERN, int S, bool WT = false, bool BUS_IN = false,
+          int DEPTH = 1>
 __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk, int ulo, int ilo,
                                              T* Qs, T* Bis, T* Bus, const Hyper<T> h,
                                              int nus = 0) {
@@ -240,12 +245,89 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
         lds_barrier();
     };
 
+    // DEPTH 2: the rows applied at step t were gathered at the start of step
+    // t-2, before the stores of steps t-2 and t-1: forward from either.
+    [[maybe_unused]] int uprev2[S];
+    [[maybe_unused]] VT pprev2[S][V];
+#pragma unroll
+    for (int x = 0; x < S; ++x) uprev2[x] = -1;
+    // step t (DEPTH 2): rows of t+2 from Tc, triples of t+4 -> Tn, apply Ra
+    auto step2 = [&](int t, Tri& Tc, Tri& Tn, Rows& Ra, Rows& Rc) __attribute__((always_inline)) {
+        unpack_gather(Tc, Rc);
+        load_tri(t + 4, Tn);
+        VT p[S][V], q[S][V];
+        T bu[S], bi[S];
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+            const bool f1 = uprev[x] == Ra.u[x];
+            const bool f2 = !f1 && uprev2[x] == Ra.u[x];
+            const VT* row = reinterpret_cast<const VT*>(Qs + (size_t)Ra.i[x] * k);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const int vi = v * GS + l;
+                const bool in = vi < kv;
+                p[x][v] = in ? (f1 ? pprev[x][v] : (f2 ? pprev2[x][v] : Ra.p[x][v])) : (VT)(T)0;
+                q[x][v] = in ? row[vi] : (VT)(T)0;
+            }
+            if constexpr (KERN != MF_RBF) {
+                bu[x] = Bus[Ra.u[x] - ulo];
+                bi[x] = Bis[Ra.i[x]];
+            } else {
+                bu[x] = bi[x] = (T)0;
+            }
+        }
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+            const T sm = group_sum<GS>(lane_partial<T, W, V, KERN>(p[x], q[x]));
+            T e, d;
+            sgd_error<T, KERN>(sm, bu[x], bi[x], Ra.r[x], h, e, d);
+            const bool lead = Ra.have[x] && l == 0;
+            if constexpr (KERN != MF_RBF) {
+                if (A.upd_user && lead) Bus[Ra.u[x] - ulo] = sgd_bias<T, KERN>(bu[x], e, d, h);
+                if (A.upd_item && lead) Bis[Ra.i[x]] = sgd_bias<T, KERN>(bi[x], e, d, h);
+            }
+            VT* pw = reinterpret_cast<VT*>(A.P + (int64_t)Ra.u[x] * k);
+            VT* qw = reinterpret_cast<VT*>(Qs + (size_t)Ra.i[x] * k);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const int vi = v * GS + l;
+                VT np, nq;
+                sgd_rows<T, KERN>(p[x][v], q[x][v], e, d, h, np, nq);
+                pprev2[x][v] = pprev[x][v];
+                pprev[x][v] = np;
+                if (!(Ra.have[x] && vi < kv)) continue;
+                if (A.upd_user) {
+                    if constexpr (WT)
+                        buf_st<16>(prs, (uint32_t)(((uint32_t)Ra.u[x] * (uint32_t)k +
+                                                    (uint32_t)(vi * W)) * sizeof(T)), np);
+                    else
+                        st<true>(pw + vi, np);
+                }
+                if (A.upd_item) qw[vi] = nq;
+            }
+            uprev2[x] = uprev[x];
+            uprev[x] = (Ra.have[x] && A.upd_user) ? Ra.u[x] : -1;
+        }
+        lds_barrier();
+    };
+
     Tri ta, tb;
     Rows ra, rb;
+    [[maybe_unused]] Tri tc;
+    [[maybe_unused]] Rows rc;
     if (nst > 0) {
-        load_tri(0, ta);
-        load_tri(1, tb);
-        unpack_gather(ta, ra);
+        if constexpr (DEPTH == 2) {
+            load_tri(0, ta);
+            load_tri(1, tb);
+            load_tri(2, tc);
+            unpack_gather(ta, ra);
+            load_tri(3, ta);
+            unpack_gather(tb, rb);
+        } else {
+            load_tri(0, ta);
+            load_tri(1, tb);
+            unpack_gather(ta, ra);
+        }
     }
     if constexpr (BUS_IN && KERN != MF_RBF) {
         // all loads issued before the first LDS write waits for them
@@ -267,9 +349,19 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
             Bus[x] = __hip_atomic_load(A.Bu + ulo + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         lds_barrier();
     }
-    for (int t = 0; t < nst; t += 2) {
-        step(t, ta, tb, ra, rb);
-        if (t + 1 < nst) step(t + 1, tb, ta, rb, ra);
+    if constexpr (DEPTH == 2) {
+        // copies by t mod 3: rows R[t%3] applied at t; triples of t+2 in
+        // T[(t+2)%3], the load of t+4 goes to T[(t+1)%3] (consumed at t-1)
+        for (int t = 0; t < nst; t += 3) {
+            step2(t, tc, tb, ra, rc);
+            if (t + 1 < nst) step2(t + 1, ta, tc, rb, ra);
+            if (t + 2 < nst) step2(t + 2, tb, ta, rc, rb);
+        }
+    } else {
+        for (int t = 0; t < nst; t += 2) {
+            step(t, ta, tb, ra, rb);
+            if (t + 1 < nst) step(t + 1, tb, ta, rb, ra);
+        }
     }
 }
 
@@ -361,7 +453,7 @@ constexpr int64_t kStrataSpinLimit = (int64_t)1 << 24;
 // cross XCDs through memory; the item slab never leaves the CU.  The result is the same sequential order as one
 // launch per stratum.  All B workgroups must be co-resident (the launcher
 // checks occupancy before choosing this kernel).
-template <typename T, int W, int GS, int V, int KERN, int S>
+template <typename T, int W, int GS, int V, int KERN, int S, int DEPTH = 1>
 __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<T> A,
                                                                     const int32_t* seq,
                                                                     int32_t n_seq, int32_t* done,
@@ -411,8 +503,8 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<
         if (s_abort) return;
         stamp(t, 1);
         // the user-bias slice is staged inside the block, behind its prologue
-        strata_block<T, W, GS, V, KERN, S, true, true>(A, (int64_t)s * B + w, ulo, ilo, Qs, Bis,
-                                                       Bus, h, nus);
+        strata_block<T, W, GS, V, KERN, S, true, true, DEPTH>(A, (int64_t)s * B + w, ulo, ilo, Qs,
+                                                              Bis, Bus, h, nus);
         __syncthreads();
         stamp(t, 2);
         if constexpr (KERN != MF_RBF) {
@@ -519,7 +611,8 @@ struct StrataRun {
         bool persistent = false;
         if ((p.flags & MF_FLAG_PERSISTENT) && p.ws &&
             p.ws_bytes >= strata_ws_bytes(p.B, p.n_seq) && a.p_bytes < 0xFFFFFFFFull) {
-            auto efn = k_sgd_strata_epoch<T, W, GS, V, KERN, S>;
+            auto efn = (p.flags & MF_FLAG_DEEP_PIPE) ? k_sgd_strata_epoch<T, W, GS, V, KERN, S, 2>
+                                                     : k_sgd_strata_epoch<T, W, GS, V, KERN, S, 1>;
             MF_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(efn),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             persistent = strata_coresident(reinterpret_cast<const void*>(efn), p.B, lds);

@@ -21,6 +21,7 @@ MF_FLAG_NT_USER = 2
 MF_FLAG_NT_ITEM = 4
 MF_FLAG_XCD_CLAIM = 8
 MF_FLAG_PERSISTENT = 16
+MF_FLAG_DEEP_PIPE = 32
 MF_ERR_CAPACITY = 3
 MF_DELTA_TAKE, MF_DELTA_APPLY = 0, 1
 KERNEL_CODES = {"linear": MF_LINEAR, "sigmoid": MF_SIGMOID, "rbf": MF_RBF}

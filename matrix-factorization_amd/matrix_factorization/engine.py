@@ -420,6 +420,17 @@ class SGDEngine:
     # one launch per epoch with the item slabs resident (MF_FLAG_PERSISTENT);
     # False: one launch per stratum
     strata_persistent = True
+    # user rows two steps ahead in the persistent sweep (MF_FLAG_DEEP_PIPE):
+    # None = by the plan, True / False forced; env MF_STRATA_DEEP=0/1 overrides
+    strata_deep_pipe: Optional[bool] = None
+
+    def _deep_pipe(self, pl) -> bool:
+        env = os.environ.get("MF_STRATA_DEEP")
+        if env in ("0", "1"):
+            return env == "1"
+        if self.strata_deep_pipe is not None:
+            return bool(self.strata_deep_pipe)
+        return False
 
     def epoch_strata(self, seq: Optional[np.ndarray], seed: int, lr: float, reg: float,
                      update_user: bool = True, update_item: bool = True, timing=False,
@@ -435,6 +446,8 @@ class SGDEngine:
         if persistent is None:
             persistent = self.strata_persistent
         flags = _lib.MF_FLAG_PERSISTENT if persistent else 0
+        if persistent and self._deep_pipe(pl):
+            flags |= _lib.MF_FLAG_DEEP_PIPE
         wsb = int(_lib.load().mf_strata_workspace_bytes(pl.B, len(seq)))
         if getattr(self, "_strata_ws", None) is None or self._strata_ws.numel() * 4 < wsb:
             # zeroed once: the error flag is sticky until check_strata() raises

@@ -168,3 +168,33 @@ def test_persistent_epoch_equals_per_stratum_launches(dtype, B):
         out.append(eng.params_numpy())
     for a, b in zip(*out):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("dtype,B,kernel,k,nu,ni", [
+    ("float64", 6, "linear", 64, 3000, 1200, ),
+    ("float32", 16, "linear", 64, 3000, 1200),
+    ("float32", 8, "sigmoid", 32, 3000, 1200),
+    ("float32", 6, "linear", 64, 200, 2000),      # ~80 ratings per user per block:
+])                                                # rows forwarded from t-1 and t-2
+def test_deep_pipe_equals_per_stratum_launches(dtype, B, kernel, k, nu, ni):
+    """MF_FLAG_DEEP_PIPE (user rows gathered two steps ahead, forwarded from
+    either of the two previous steps of the slot) keeps the sequential order:
+    bit-identical to one launch per stratum, user-only epochs included."""
+    nnz = 150000 if nu > 1000 else 100000
+    u, i, r = _synthetic(61, nu, ni, nnz)
+    rs = np.random.RandomState(62)
+    P = rs.normal(0, 0.1, (nu, k)); Q = rs.normal(0, 0.1, (ni, k))
+    bu = rs.normal(0, 0.1, nu); bi = rs.normal(0, 0.1, ni)
+    out = []
+    for deep in (True, None):
+        eng = _engine(u, i, r, nu, ni, k, kernel, dtype, P, Q, bu, bi)
+        eng.prepare_strata(n_blocks=B)
+        eng.strata_deep_pipe = deep
+        for ep in range(3):
+            seq = np.random.RandomState(ep).permutation(B).astype(np.int32)
+            eng.epoch_strata(seq, 2000 + ep, lr=0.01, reg=0.02, update_item=ep != 2,
+                             persistent=deep is True)
+        eng.check_strata()
+        out.append(eng.params_numpy())
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
