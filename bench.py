@@ -412,14 +412,14 @@ def main() -> int:
     phase = not args.no_phase_timing
     launches_per_epoch = nb if strata else int(np.sum(np.diff(eng.colored) > 0))
     persistent = False
-    events = []     # (sgd start, sgd end, sse end) per timed epoch
+    events = []     # (sgd start, sgd end, exchange end, sse end) per timed epoch
 
     def epoch(ep, timed):
         # hipEvents on the stream the kernels run on (torch's current stream,
         # which the engine launches on): one pair around the epoch's SGD
         # launches, one more after the RMSE pass -- no host sync in the loop.
         seq = seq_for(ep)
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if (timed and phase) else None
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if (timed and phase) else None
         if exch is not None:
             exch.begin_epoch()
         if ev:
@@ -429,9 +429,11 @@ def main() -> int:
             ev[1].record()
         if exch is not None:
             exch.end_epoch()
-        eng.sse_async(ep)
         if ev:
             ev[2].record()
+        eng.sse_async(ep)
+        if ev:
+            ev[3].record()
             events.append(ev)
 
     for ep in range(args.warmup):
@@ -497,7 +499,8 @@ def main() -> int:
         phases = None
         if events:
             sgd_s = sum(e[0].elapsed_time(e[1]) for e in events) / 1e3
-            sse_s = sum(e[1].elapsed_time(e[2]) for e in events) / 1e3
+            exch_s = sum(e[1].elapsed_time(e[2]) for e in events) / 1e3
+            sse_s = sum(e[2].elapsed_time(e[3]) for e in events) / 1e3
             launches = launches_per_epoch * len(events)
             alg = alg_epoch * len(events)                           # algorithmic bytes
             achieved = alg / sgd_s / 1e9
@@ -521,6 +524,7 @@ def main() -> int:
             }
             phases = {"sgd_ms_per_epoch": sgd_s / len(events) * 1e3,
                       "rmse_ms_per_epoch": sse_s / len(events) * 1e3,
+                      "exchange_ms_per_epoch": exch_s / len(events) * 1e3,
                       "sgd_updates_per_s": n_local * len(events) / sgd_s}
         out = {
             "metric": METRIC, "value": value, "unit": "rating-updates/s",
