@@ -622,7 +622,7 @@ __global__ __launch_bounds__(kBlock) void k_sse_owned(ReadArgs<T> A, SliceTab SL
 
 __global__ void k_sum_partials(const double* part, int n, double* out);
 
-constexpr int kSseMaxBlocks = 2048;
+constexpr int kSseMaxBlocks = 8192;
 
 // ------------------------------------------------ (dtype, k) -> row layout
 // Calls F.template run<W, GS, V, KERN>() for dtype T.
@@ -813,9 +813,14 @@ struct SseRun {
         a.Bu = static_cast<const T*>(p.bu); a.Bi = static_cast<const T*>(p.bi);
         a.n = p.n; a.k = p.k; a.bound = 0; a.out = nullptr; a.partials = p.partials;
         a.h = make_hyper<T>(p.mu, 0.0, 0.0, p.gamma, p.lo, p.hi);
-        // One wave of workgroups: every resident slot gets one equal share of
-        // its slice (a second, partial round of workgroups would leave the
-        // chip part idle for a whole share).  MF_SSE_BLOCKS overrides (probes).
+        // Up to eight workgroups per resident slot, each an equal share of
+        // its slice, but at least ~6K ratings per wave: the shorter shares
+        // even out the per-wave rate differences on large inputs (C3, rank
+        // 64: 2.45 ms with one share per resident slot, 2.26 / 2.25 / 2.24 ms
+        // with 2048 / 4096 / 8192 workgroups; tools/sse_probe.py), while on
+        // small ones (C2, the N=8 shard) more workgroups only add tail
+        // (0.094 -> 0.105 ms, 0.276 -> 0.286 ms at 8 per slot).
+        // MF_SSE_BLOCKS overrides (probes).
         a.p_bytes = (uint64_t)p.n_users * p.k * sizeof(T);
         a.q_bytes = (uint64_t)p.n_items * p.k * sizeof(T);
         a.bu_bytes = (uint64_t)p.n_users * sizeof(T);
@@ -851,7 +856,11 @@ struct SseRun {
             else
                 resident = kSseMaxBlocks;
         }
-        int blocks = std::min(resident, kSseMaxBlocks);
+        constexpr int64_t kSseRatingsPerWave = 6144;
+        const int64_t by_size = p.n / (kSseRatingsPerWave * kWavesPerBlock);
+        int blocks = (int)std::min<int64_t>(
+            std::max<int64_t>(resident, std::min<int64_t>(by_size, 8 * (int64_t)resident)),
+            kSseMaxBlocks);
         if (const char* e = std::getenv("MF_SSE_BLOCKS")) {
             const int v = std::atoi(e);
             if (v > 0) blocks = std::min(v, kSseMaxBlocks);
