@@ -524,8 +524,9 @@ def main() -> int:
             }
             phases = {"sgd_ms_per_epoch": sgd_s / len(events) * 1e3,
                       "rmse_ms_per_epoch": sse_s / len(events) * 1e3,
-                      "exchange_ms_per_epoch": exch_s / len(events) * 1e3,
                       "sgd_updates_per_s": n_local * len(events) / sgd_s}
+            if world > 1:
+                phases["exchange_ms_per_epoch"] = exch_s / len(events) * 1e3
         out = {
             "metric": METRIC, "value": value, "unit": "rating-updates/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
