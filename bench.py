@@ -24,10 +24,13 @@ Also reported (rank 0):
                 equivalent rate reported beside it.  `traffic` = measured HBM
                 bytes per launch from rocprofv3 PMC (profiles/) or null;
   cpu_baseline  the CPU oracle (FP64 C port of the reference loop, 1 core)
-                on a bounded sample: the first strata (colours) of epoch 1
-                (~10M ratings by default), SGD + RMSE over the sample;
-  parity        GPU (FP32) vs oracle (FP64) after that same partial epoch
-                from the same initial state: RMSE over the sample.
+                timed on one full epoch (SGD sweep + RMSE pass) of the same
+                workload, with the host's CPU model and nproc;
+  parity        from the same initial state, after one full epoch: GPU
+                (FP32) vs oracle (FP64) in the GPU's serialised order, and the
+                oracle in the GPU's order vs the oracle in the reference's own
+                np.random.shuffle order, next to the reference's own
+                shuffle-seed spread (two shuffle seeds) -- see cpu_leg().
 """
 
 from __future__ import annotations
@@ -141,12 +144,13 @@ def run_als(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
 
     # ---- CPU baseline + parity: the user half-sweep for a prefix of users
     cpu_baseline = parity = None
-    if args.cpu_sample > 0:
+    if args.cpu_sample != 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle  # test infrastructure: checker and reported baseline only
 
         deg = np.bincount(u, minlength=nu)
-        n_s = int(np.searchsorted(np.cumsum(deg), min(args.cpu_sample, 1_000_000, nnz))) + 1
+        want = 1_000_000 if args.cpu_sample < 0 else min(args.cpu_sample, 1_000_000)
+        n_s = int(np.searchsorted(np.cumsum(deg), min(want, nnz))) + 1
         n_s = min(n_s, nu)
         sel = u < n_s
         reset()
@@ -235,6 +239,131 @@ def run_als(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
     return 0
 
 
+def host_info() -> dict:
+    """The host the CPU leg ran on (print nproc and the model)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        nproc = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        nproc = None
+    return {"cpu_model": model, "nproc": nproc, "os_cpu_count": os.cpu_count()}
+
+
+def cpu_leg(args, eng, run, serial, seq_for, rot_for, reset_params, strat_sizes, nb, strata,
+            kernel, k, mu, P0, Q0, nu, ni, n_local):
+    """CPU baseline + parity, untimed, before the timed epochs.
+
+    Full epoch (--cpu-sample -1, the default).  From the same initial state
+    (P0, Q0, zero biases) the GPU runs epoch 1 (FP32, strata order), then the
+    FP64 oracle (oracle/mf_oracle.c, the reference's per-rating arithmetic)
+    runs three full epochs on the host:
+      (a) in the GPU's serialised order (StrataPlan.serial_order): GPU vs
+          oracle, |dRMSE|, max|dP|, max|dQ|; timed alone = cpu_baseline;
+      (b) in the reference's own order, np.random.shuffle of the rows
+          (kernel_matrix_factorization.py:369-371, :428-440): |RMSE(a) -
+          RMSE(b)| against the north-star 1e-5;
+      (c) as (b) with another shuffle seed: the reference's own
+          seed-to-seed spread at this size, the yardstick for (b).
+    (b) and (c) run concurrently in two threads (ctypes drops the GIL).
+    --cpu-sample N > 0: the first strata of epoch 1 covering >= N ratings,
+    (a) only."""
+    import concurrent.futures as cf
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # test infrastructure: checker and reported baseline only
+
+    hyp = dict(kernel=kernel, gamma=1.0 / k, min_rating=1.0, max_rating=5.0)
+    unit_name = "strata" if strata else "colours"
+    seq0 = seq_for(0)
+    full = args.cpu_sample < 0
+    if full:
+        m = nb
+    else:
+        sizes = strat_sizes[seq0]
+        m = min(int(np.searchsorted(np.cumsum(sizes), min(args.cpu_sample, n_local))) + 1, nb)
+    reset_params()
+    run(0, seq0[:m])
+    eng.sse_async(0)
+    rmse_gpu_kernel = eng.rmse_values(1)[0] if full else None
+    Pg, Qg, bug, big = eng.params_numpy()
+    order = serial(0, seq0[:m])
+    S = len(order)
+    if full:
+        u, i, r = eng.u_host, eng.i_host, eng.r_host.astype(np.float64)
+    else:   # the sample's ratings only, in the serialised order
+        u, i, r = eng.u_host[order], eng.i_host[order], eng.r_host[order].astype(np.float64)
+        order = None
+
+    def state():
+        return (np.zeros(nu), np.zeros(ni), P0.astype(np.float64), Q0.astype(np.float64))
+
+    def epoch(order_):
+        bu, bi, P, Q = state()
+        t0 = time.perf_counter()
+        oracle.sgd_pass(u, i, r, mu, bu, bi, P, Q, lr=args.lr, reg=args.reg, order=order_,
+                        **hyp)
+        t1 = time.perf_counter()
+        sse = oracle.sse(u, i, r, mu, bu, bi, P, Q, **hyp)
+        t2 = time.perf_counter()
+        return (bu, bi, P, Q), float(np.sqrt(sse / len(u))), t1 - t0, t2 - t1
+
+    log(f"cpu oracle (a): {S} ratings ({m} of {nb} {unit_name}, GPU serial order), FP64, "
+        f"1 thread")
+    (bu, bi, P, Q), rm_a, t_sgd, t_sse = epoch(order)
+    rm_g = float(np.sqrt(oracle.sse(u, i, r, mu, bug, big, Pg, Qg, **hyp) / len(u)))
+    host = host_info()
+    what = (f"one full epoch (all {S} ratings)" if full
+            else f"first {m} of {nb} {unit_name} of epoch 1 = {S} ratings")
+    cpu_baseline = {
+        "value": S / (t_sgd + t_sse), "unit": "rating-updates/s", "cores": 1, "kind": "port",
+        "sample": (f"{what} of the same workload: FP64 sequential SGD sweep ({t_sgd:.1f}s) "
+                   f"+ RMSE pass ({t_sse:.1f}s), oracle/mf_oracle.c, one thread"),
+        "sgd_only": S / t_sgd, **host,
+    }
+    parity = {
+        "what": (f"{what} from the same initial state: (a) GPU FP32 strata vs CPU oracle "
+                 f"FP64 in the GPU's serialised order"
+                 + ("; (b) oracle in the reference's np.random.shuffle order; (c) the same, "
+                    "another shuffle seed (the reference's own seed spread)" if full else "")),
+        "rmse_gpu": rm_g, "rmse_cpu": rm_a, "abs_diff": abs(rm_g - rm_a),
+        "max_abs_dP": float(np.max(np.abs(Pg - P))),
+        "max_abs_dQ": float(np.max(np.abs(Qg - Q))),
+        "max_abs_dbu": float(np.max(np.abs(bug - bu))),
+        "max_abs_dbi": float(np.max(np.abs(big - bi))),
+    }
+    del P, Q, bu, bi
+    if full:
+        parity["rmse_gpu_kernel"] = rmse_gpu_kernel      # k_sse_owned's own FP64 reduction
+        parity["abs_diff_gpu_kernel"] = abs(rmse_gpu_kernel - rm_a)
+
+        def shuffled(seed):
+            o = np.arange(len(u), dtype=np.int64)
+            np.random.RandomState(seed).shuffle(o)       # = np.random.shuffle(X), :371
+            return epoch(o)[1]
+
+        log("cpu oracle (b), (c): the same epoch in two np.random.shuffle orders, 2 threads")
+        with cf.ThreadPoolExecutor(2) as ex:
+            rm_b, rm_c = ex.map(shuffled, (7, 8))
+        parity.update({
+            "rmse_shuffle_order": rm_b, "rmse_shuffle_order_seed2": rm_c,
+            "abs_diff_strata_vs_shuffle": abs(rm_a - rm_b),
+            "shuffle_seed_spread": abs(rm_b - rm_c),
+            "gate_1e5": bool(abs(rm_a - rm_b) <= 1e-5 and abs(rm_g - rm_a) <= 1e-5),
+        })
+    log(f"cpu {cpu_baseline['value'] / 1e6:.2f} M/s; parity " +
+        ", ".join(f"{kk}={vv:.3e}" for kk, vv in parity.items()
+                  if isinstance(vv, float) and kk.startswith(("abs", "shuffle"))))
+    return cpu_baseline, parity
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -246,8 +375,10 @@ def main() -> int:
     ap.add_argument("--reg", type=float, default=None,
                     help="default 0.02 for SGD (project_template/pipeline/train.py:29-36), "
                          "1.0 for ALS (KernelMF's default reg)")
-    ap.add_argument("--cpu-sample", type=int, default=10_000_000,
-                    help="ratings in the CPU-oracle sample (0 = skip the CPU leg)")
+    ap.add_argument("--cpu-sample", type=int, default=-1,
+                    help="CPU leg: -1 = one full epoch (default; parity in the strata "
+                         "order and in the reference's shuffle order), N > 0 = the first "
+                         "strata of epoch 1 covering >= N ratings, 0 = skip")
     ap.add_argument("--no-phase-timing", action="store_true",
                     help="do not bracket the SGD / RMSE phases with hipEvents")
     ap.add_argument("--blocks", type=int, default=None,
@@ -356,56 +487,13 @@ def main() -> int:
         return np.concatenate([np.arange(eng.colored[b], eng.colored[b + 1])
                                for b in seq]).astype(np.int64)
 
-    # ---------------- CPU baseline + parity on a bounded sample (rank 0, N=1)
+    # ---------------- CPU baseline + parity (rank 0, N=1; untimed)
     cpu_baseline = None
     parity = None
-    if world == 1 and args.cpu_sample > 0:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle  # test infrastructure: checker and reported baseline only
-
-        seq0 = seq_for(0)
-        sizes = strat_sizes[seq0]
-        m = int(np.searchsorted(np.cumsum(sizes), min(args.cpu_sample, n_local))) + 1
-        m = min(m, nb)
-        reset_params()
-        run(0, seq0[:m])
-        Pg, Qg, bug, big = eng.params_numpy()
-        order = serial(0, seq0[:m])
-        S = len(order)
-        us, is_, rsmp = eng.u_host[order], eng.i_host[order], eng.r_host[order].astype(np.float64)
-        P = P0.astype(np.float64)
-        Q = Q0.astype(np.float64)
-        bu = np.zeros(nu)
-        bi = np.zeros(ni)
-        unit_name = "strata" if strata else "colours"
-        log(f"cpu oracle: {S} ratings ({m} {unit_name}), FP64, 1 thread")
-        t0 = time.perf_counter()
-        oracle.sgd_pass(us, is_, rsmp, mu, bu, bi, P, Q, kernel=kernel, gamma=1.0 / k,
-                        lr=args.lr, reg=args.reg, min_rating=1.0, max_rating=5.0)
-        t_sgd = time.perf_counter() - t0
-        t0 = time.perf_counter()
-        sse_cpu = oracle.sse(us, is_, rsmp, mu, bu, bi, P, Q, kernel=kernel,
-                             gamma=1.0 / k, min_rating=1.0, max_rating=5.0)
-        t_sse = time.perf_counter() - t0
-        sse_gpu = oracle.sse(us, is_, rsmp, mu, bug, big, Pg, Qg, kernel=kernel,
-                             gamma=1.0 / k, min_rating=1.0, max_rating=5.0)
-        rm_c, rm_g = float(np.sqrt(sse_cpu / S)), float(np.sqrt(sse_gpu / S))
-        cpu_baseline = {
-            "value": S / (t_sgd + t_sse), "unit": "rating-updates/s", "cores": 1,
-            "kind": "port",
-            "sample": (f"first {m} of {nb} {unit_name} of epoch 1 = {S} ratings of the same "
-                       f"workload: FP64 sequential SGD sweep ({t_sgd:.1f}s) + RMSE pass "
-                       f"({t_sse:.1f}s), oracle/mf_oracle.c"),
-            "sgd_only": S / t_sgd,
-        }
-        parity = {
-            "what": "RMSE over the sample after the same partial epoch from the same "
-                    "initial state: GPU FP32 vs CPU oracle FP64",
-            "rmse_gpu": rm_g, "rmse_cpu": rm_c, "abs_diff": abs(rm_g - rm_c),
-            "max_abs_dP": float(np.max(np.abs(Pg - P))),
-            "max_abs_dQ": float(np.max(np.abs(Qg - Q))),
-        }
-        log(f"cpu {cpu_baseline['value'] / 1e6:.2f} M/s; parity |drmse|={parity['abs_diff']:.2e}")
+    if world == 1 and args.cpu_sample != 0:
+        cpu_baseline, parity = cpu_leg(args, eng, run, serial, seq_for, rot_for, reset_params,
+                                       strat_sizes, nb, strata, kernel, k, mu, P0, Q0, nu, ni,
+                                       n_local)
 
     # ---------------- warmup + timed epochs
     reset_params()

@@ -60,8 +60,11 @@ enum {
                                  launch, item slabs resident in LDS (needs
                                  `workspace`; falls back to one launch per
                                  stratum when the grid cannot be co-resident) */
-    MF_FLAG_DEEP_PIPE = 32    /* with MF_FLAG_PERSISTENT: user rows gathered two
+    MF_FLAG_DEEP_PIPE = 32,   /* with MF_FLAG_PERSISTENT: user rows gathered two
                                  steps ahead (blocks of few steps)               */
+    MF_FLAG_NO_COOP = 64      /* with MF_FLAG_PERSISTENT: plain launch instead of
+                                 hipLaunchCooperativeKernel (diagnostic A/B; the
+                                 occupancy check is then the only guard)         */
 };
 
 const char* mf_last_error(void);
@@ -163,6 +166,33 @@ int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_ids,
                         double max_rating, int32_t update_user_params,
                         int32_t update_item_params, int32_t flags, void* workspace,
                         size_t workspace_bytes, void* stream, double* kernel_ms);
+/*
+ * The same epoch in DELTA-OUT form, for user-sharded data parallelism (every
+ * rank holds a replica of the item rows and biases; no
+ * counterpart in the single-process reference): item_features / item_biases
+ * are left at their values before the call, and item_delta (DEVICE, n_items
+ * x n_factors) / item_bias_delta (DEVICE, n_items; unused by rbf) receive
+ * the local update (value after the epoch - value before).  The caller
+ * all-reduces the deltas and adds the sum (mf_replica_delta, MF_DELTA_APPLY).
+ * The persistent kernel writes the delta where it would write the slab back;
+ * the per-stratum fallback keeps the start values in the delta buffers and
+ * swaps at the end.  User rows and biases are updated in place as usual.
+ */
+int mf_sgd_epoch_strata_delta(const int32_t* user_ids, const int32_t* item_ids,
+                              const void* ratings, int64_t n_positions, int32_t n_blocks,
+                              const int32_t* user_bounds, const int32_t* item_bounds,
+                              const int64_t* block_steps, int32_t n_slots,
+                              int32_t max_block_items, int32_t max_block_users,
+                              const int32_t* strata_seq, int32_t n_seq, uint32_t seed,
+                              double global_mean, void* user_biases, void* item_biases,
+                              void* user_features, void* item_features, int32_t n_users,
+                              int32_t n_items, int32_t n_factors, int32_t kernel,
+                              int32_t dtype, double gamma, double lr, double reg,
+                              double min_rating, double max_rating,
+                              int32_t update_user_params, int32_t update_item_params,
+                              int32_t flags, void* workspace, size_t workspace_bytes,
+                              void* item_delta, void* item_bias_delta, void* stream,
+                              double* kernel_ms);
 size_t mf_strata_workspace_bytes(int32_t n_blocks, int32_t n_seq);
 /* Synchronises `stream` and reports whether a persistent strata sweep using
  * `workspace` gave up waiting (MF_ERR_HIP) since the workspace was zeroed. */
@@ -221,10 +251,15 @@ int mf_predict(const int32_t* user_ids, const int32_t* item_ids,
 /*
  * Top-`amount` items for each of n_query users (scores = unbounded
  * prediction of every item, as recommend() scores them,
- * recommender_base.py:245-260).  Items flagged in the optional device mask
- * exclude[q * n_items + i] != 0 are skipped.  Ties are broken by the lower
- * item id.  out_items (int32) / out_scores (dtype): device, n_query * amount.
- * Rows with fewer than `amount` candidates are padded with id -1.
+ * recommender_base.py:245-260).  Exclusions (recommend's items_known,
+ * :245-250) as a DEVICE CSR list, both nullable: the items
+ * exclude_items[exclude_ptr[q] .. exclude_ptr[q+1]) (int32, any order; ids
+ * outside [0, n_items) ignored) are skipped for query q.  Ties are broken by
+ * the lower item id (the order a stable sort_values gives; the reference's
+ * default quicksort leaves tie order unspecified, :259).  out_items (int32) /
+ * out_scores (dtype): device, n_query * amount.  Rows with fewer than
+ * `amount` candidates are padded with id -1.  The workspace grows with
+ * n_query * n_items: callers chunk the users.
  * workspace: device, >= mf_topk_workspace_bytes(n_query, n_items, amount).
  */
 size_t mf_topk_workspace_bytes(int32_t n_query, int32_t n_items,
@@ -234,7 +269,8 @@ int mf_topk(const int32_t* query_users, int32_t n_query, double global_mean,
             const void* user_features, const void* item_features,
             int32_t n_items, int32_t n_factors, int32_t kernel, int32_t dtype,
             double gamma, double min_rating, double max_rating,
-            const uint8_t* exclude, int32_t amount, void* workspace,
+            const int64_t* exclude_ptr, const int32_t* exclude_items,
+            int32_t amount, void* workspace,
             int32_t* out_items, void* out_scores, void* stream);
 
 /* ---------------- BaselineModel (bias-only), baseline_model.py ---------- */
@@ -442,6 +478,11 @@ int mf_factorize(const int64_t* vals, int64_t n, int64_t* codes, int64_t* unique
                  int64_t* n_uniques);
 int mf_gather(const void* src, int64_t n_src, int32_t elem_bytes, const int64_t* idx, int64_t n,
               void* dst);
+/* 64-bit fingerprint of a HOST buffer (threaded, not cryptographic): lets the
+ * estimator tell whether the device copy of a parameter array is still the
+ * NumPy attribute's content (the reference predicts from the live arrays,
+ * kernel_matrix_factorization.py:148-160). */
+uint64_t mf_fingerprint(const void* data, int64_t n_bytes);
 
 #ifdef __cplusplus
 }

@@ -328,3 +328,46 @@ extern "C" int mf_gather(const void* src, int64_t n_src, int32_t elem_bytes, con
     }
     return MF_OK;
 }
+
+// Fingerprint of a host buffer (KernelMF._predictor: are the device copies of
+// P / Q / b_u / b_i still those of the NumPy attributes, in-place edits
+// included?).  Chunks of 64-bit words are folded with the splitmix64
+// multiply-rotate lanes on the host threads (splitmix64 finaliser per
+// chunk); the chunk hashes are combined in order.  Not
+// cryptographic: equal buffers give equal values, a changed word changes the
+// value with overwhelming probability.
+extern "C" uint64_t mf_fingerprint(const void* data, int64_t n_bytes) {
+    if (!data || n_bytes <= 0) return 0x9E3779B97F4A7C15ull ^ (uint64_t)n_bytes;
+    const unsigned char* b = static_cast<const unsigned char*>(data);
+    const int64_t nw = n_bytes / 8;
+    const int T = host_threads();
+    const int C = std::max(1, std::min<int>(4 * T, (int)(nw >> 16) + 1));   // chunks
+    std::vector<uint64_t> part((size_t)C, 0);
+    for_buckets(C, T, [&](int c) {
+        const int64_t lo = nw * c / C, hi = nw * (c + 1) / C;
+        // four independent multiply-rotate lanes (memory-bound, not latency-bound)
+        constexpr uint64_t K = 0x9FB21C651E98DF25ull;
+        uint64_t h[4] = {0x243F6A8885A308D3ull + (uint64_t)c, 0x13198A2E03707344ull,
+                         0xA4093822299F31D0ull, 0x082EFA98EC4E6C89ull};
+        int64_t w = lo;
+        for (; w + 3 < hi; w += 4) {
+            uint64_t x[4];
+            std::memcpy(x, b + 8 * w, 32);
+            for (int j = 0; j < 4; ++j) {
+                const uint64_t y = h[j] ^ x[j];
+                h[j] = ((y << 29) | (y >> 35)) * K;
+            }
+        }
+        for (; w < hi; ++w) {
+            uint64_t x;
+            std::memcpy(&x, b + 8 * w, 8);
+            h[0] = mix64(h[0] ^ x);
+        }
+        const uint64_t h0 = mix64(h[0] ^ mix64(h[1])), h1 = mix64(h[2] ^ mix64(h[3]));
+        part[(size_t)c] = mix64(h0 ^ (h1 * 0x9E3779B97F4A7C15ull));
+    });
+    uint64_t h = (uint64_t)n_bytes;
+    for (int c = 0; c < C; ++c) h = mix64(h ^ part[(size_t)c]) + (uint64_t)c;
+    for (int64_t t = nw * 8; t < n_bytes; ++t) h = mix64(h ^ b[t]);
+    return h;
+}

@@ -296,7 +296,7 @@ extern "C" int32_t mf_strata_slots(int32_t n_factors, int32_t dtype) {
     return dispatch_rows<double>(n_factors, MF_LINEAR, f);
 }
 
-extern "C" int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_ids,
+static int strata_epoch(const int32_t* user_ids, const int32_t* item_ids,
                                    const void* ratings, int64_t n_positions, int32_t n_blocks,
                                    const int32_t* user_bounds, const int32_t* item_bounds,
                                    const int64_t* block_steps, int32_t n_slots,
@@ -309,7 +309,7 @@ extern "C" int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_
                                    double min_rating, double max_rating,
                                    int32_t update_user_params, int32_t update_item_params,
                                    int32_t flags, void* workspace, size_t workspace_bytes,
-                                   void* stream, double* kernel_ms) {
+                                   void* stream, double* kernel_ms, void* dq, void* dbi) {
     if (n_positions < 0 || n_blocks < 0 || n_seq < 0 || n_users < 0 || n_items < 0 ||
         max_block_items < 0 || max_block_users < 0 || n_slots < 1) {
         set_error("negative size");
@@ -342,11 +342,58 @@ extern "C" int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_
                    user_features, item_features, n_factors, kernel, gamma, lr, reg,
                    min_rating, max_rating, update_user_params ? 1 : 0,
                    update_item_params ? 1 : 0, flags, workspace, workspace_bytes, n_users,
-                   (hipStream_t)stream, kernel_ms};
+                   (hipStream_t)stream, kernel_ms, n_items, dq, dbi};
     if (dtype == MF_F32) return strata_launch_f32(P);
     if (dtype == MF_F64) return strata_launch_f64(P);
     set_error("unknown dtype code %d", dtype);
     return MF_ERR_INVALID;
+}
+
+extern "C" int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_ids,
+                                   const void* ratings, int64_t n_positions, int32_t n_blocks,
+                                   const int32_t* user_bounds, const int32_t* item_bounds,
+                                   const int64_t* block_steps, int32_t n_slots,
+                                   int32_t max_block_items, int32_t max_block_users,
+                                   const int32_t* strata_seq, int32_t n_seq, uint32_t seed,
+                                   double global_mean, void* user_biases, void* item_biases,
+                                   void* user_features, void* item_features, int32_t n_users,
+                                   int32_t n_items, int32_t n_factors, int32_t kernel,
+                                   int32_t dtype, double gamma, double lr, double reg,
+                                   double min_rating, double max_rating,
+                                   int32_t update_user_params, int32_t update_item_params,
+                                   int32_t flags, void* workspace, size_t workspace_bytes,
+                                   void* stream, double* kernel_ms) {
+    return strata_epoch(user_ids, item_ids, ratings, n_positions, n_blocks, user_bounds,
+                        item_bounds, block_steps, n_slots, max_block_items, max_block_users,
+                        strata_seq, n_seq, seed, global_mean, user_biases, item_biases,
+                        user_features, item_features, n_users, n_items, n_factors, kernel, dtype,
+                        gamma, lr, reg, min_rating, max_rating, update_user_params,
+                        update_item_params, flags, workspace, workspace_bytes, stream, kernel_ms,
+                        nullptr, nullptr);
+}
+
+extern "C" int mf_sgd_epoch_strata_delta(
+    const int32_t* user_ids, const int32_t* item_ids, const void* ratings, int64_t n_positions,
+    int32_t n_blocks, const int32_t* user_bounds, const int32_t* item_bounds,
+    const int64_t* block_steps, int32_t n_slots, int32_t max_block_items,
+    int32_t max_block_users, const int32_t* strata_seq, int32_t n_seq, uint32_t seed,
+    double global_mean, void* user_biases, void* item_biases, void* user_features,
+    void* item_features, int32_t n_users, int32_t n_items, int32_t n_factors, int32_t kernel,
+    int32_t dtype, double gamma, double lr, double reg, double min_rating, double max_rating,
+    int32_t update_user_params, int32_t update_item_params, int32_t flags, void* workspace,
+    size_t workspace_bytes, void* item_delta, void* item_bias_delta, void* stream,
+    double* kernel_ms) {
+    if (!item_delta || (kernel != MF_RBF && !item_bias_delta)) {
+        set_error("mf_sgd_epoch_strata_delta: NULL delta buffer");
+        return MF_ERR_INVALID;
+    }
+    return strata_epoch(user_ids, item_ids, ratings, n_positions, n_blocks, user_bounds,
+                        item_bounds, block_steps, n_slots, max_block_items, max_block_users,
+                        strata_seq, n_seq, seed, global_mean, user_biases, item_biases,
+                        user_features, item_features, n_users, n_items, n_factors, kernel, dtype,
+                        gamma, lr, reg, min_rating, max_rating, update_user_params,
+                        update_item_params, flags, workspace, workspace_bytes, stream, kernel_ms,
+                        item_delta, item_bias_delta);
 }
 
 extern "C" size_t mf_sse_workspace_bytes(int64_t n_ratings) {

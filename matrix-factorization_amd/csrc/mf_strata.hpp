@@ -70,6 +70,8 @@ struct StrataArgs {
     int32_t upd_user;
     int32_t upd_item;
     uint64_t p_bytes;        // bytes of P (write-through buffer stores: < 4 GiB)
+    T* Dq;                   // nullable: delta-out mode (persistent kernel): the epoch
+    T* Dbi;                  //   leaves Q / Bi untouched and writes Dq = Q' - Q, Dbi
     Hyper<T> h;
     int64_t* probe;          // nullable: persistent-kernel phase stamps (mf_strata_set_probe)
 };
@@ -396,6 +398,40 @@ __device__ __forceinline__ void strata_store_slab(const StrataArgs<T>& A, int il
         for (int t = threadIdx.x; t < nqi; t += kStrataThreads) A.Bi[ilo + t] = Bis[t];
 }
 
+// Delta-out end of the persistent epoch (user-sharded multi-GPU): Q and Bi
+// were not written during the epoch (the slab lived in LDS), so the local
+// update of this slab is LDS - global; it goes to Dq / Dbi and the replica
+// stays at its start-of-epoch value for the exchange to update.
+template <typename T, int W, int KERN>
+__device__ __forceinline__ void strata_delta_slab(const StrataArgs<T>& A, int ilo, int nqi,
+                                                  const T* Qs, const T* Bis) {
+    using VT = typename VecOf<T, W>::type;
+    const int k = A.k;
+    const VT* q0 = reinterpret_cast<const VT*>(A.Q + (int64_t)ilo * k);
+    VT* dst = reinterpret_cast<VT*>(A.Dq + (int64_t)ilo * k);
+    const VT* src = reinterpret_cast<const VT*>(Qs);
+    const int nv = nqi * (k / W);
+#pragma unroll 4
+    for (int t = threadIdx.x; t < nv; t += kStrataThreads) dst[t] = src[t] - q0[t];
+    if constexpr (KERN != MF_RBF)
+        for (int t = threadIdx.x; t < nqi; t += kStrataThreads)
+            A.Dbi[ilo + t] = Bis[t] - A.Bi[ilo + t];
+}
+
+// Fallback form of delta-out (one launch per stratum writes Q as it goes):
+// before the strata D holds a copy of the start values S, after them cur
+// holds the new values X; this leaves cur = S, D = X - S.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_delta_swap(T* __restrict__ cur, T* __restrict__ d,
+                                                       int64_t n) {
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < n;
+         j += (int64_t)gridDim.x * kBlock) {
+        const T x = cur[j], s0 = d[j];
+        cur[j] = s0;
+        d[j] = x - s0;
+    }
+}
+
 __device__ __forceinline__ Hyper<float> hyper_regs(const Hyper<float>& s) {
     // field by field: an aggregate copy of the kernel-argument struct ends up
     // in scratch once the step lambdas capture it
@@ -451,8 +487,10 @@ constexpr int64_t kStrataSpinLimit = (int64_t)1 << 24;
 // store; the consumer polls relaxed and reads every handed-off byte with sc1
 // loads (L2-served), so no fence is needed on either side.  The user rows
 // cross XCDs through memory; the item slab never leaves the CU.  The result is the same sequential order as one
-// launch per stratum.  All B workgroups must be co-resident (the launcher
-// checks occupancy before choosing this kernel).
+// launch per stratum.  All B workgroups must be co-resident: the launcher
+// checks occupancy, then launches cooperatively (hipLaunchCooperativeKernel:
+// the runtime refuses a grid that cannot be resident at once, and the epoch
+// then runs as one launch per stratum).
 template <typename T, int W, int GS, int V, int KERN, int S, int DEPTH = 1>
 __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<T> A,
                                                                     const int32_t* seq,
@@ -522,7 +560,10 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<
         stamp(t, 3);
     }
     __syncthreads();
-    strata_store_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
+    if (A.Dq)
+        strata_delta_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
+    else
+        strata_store_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
 }
 
 // diagnostic: device buffer for the persistent kernel's phase stamps
@@ -538,6 +579,7 @@ struct StrataParams {
     double gamma, lr, reg, lo, hi; int32_t uu, ui, flags;
     void* ws; size_t ws_bytes; int64_t n_users;
     hipStream_t stream; double* kernel_ms;
+    int64_t n_items; void* dq; void* dbi;    // delta-out (nullable)
 };
 
 // workspace of the persistent kernel: done[B], err, seq[n_seq] (int32)
@@ -600,6 +642,12 @@ struct StrataRun {
         a.ubnd = p.ubnd; a.ibnd = p.ibnd; a.bstep = p.bstep;
         a.B = p.B; a.seed = p.seed; a.k = p.k; a.upd_user = p.uu; a.upd_item = p.ui;
         a.p_bytes = (uint64_t)p.n_users * (uint64_t)p.k * sizeof(T);
+        a.Dq = static_cast<T*>(p.dq);
+        a.Dbi = static_cast<T*>(p.dbi);
+        if (p.dq && !p.dbi && KERN != MF_RBF) {
+            set_error("delta-out needs both the item-row and the item-bias delta buffers");
+            return MF_ERR_INVALID;
+        }
         a.h = make_hyper<T>(p.mu, p.lr, p.reg, p.gamma, p.lo, p.hi);
         a.probe = strata_probe_ptr();
         hipEvent_t ev[2] = {nullptr, nullptr};
@@ -619,19 +667,51 @@ struct StrataRun {
             if (persistent) {
                 int32_t* done = static_cast<int32_t*>(p.ws);
                 int32_t* err = done + p.B;
-                int32_t* dseq = err + 1;
+                const int32_t* dseq = err + 1;
+                int32_t nseq = p.n_seq;
                 MF_HIP_CHECK(hipMemsetAsync(done, 0, sizeof(int32_t) * (size_t)p.B, p.stream));
-                MF_HIP_CHECK(hipMemcpyAsync(dseq, p.seq, sizeof(int32_t) * (size_t)p.n_seq,
+                MF_HIP_CHECK(hipMemcpyAsync(err + 1, p.seq, sizeof(int32_t) * (size_t)p.n_seq,
                                             hipMemcpyHostToDevice, p.stream));
-                hipLaunchKernelGGL(efn, dim3((unsigned)p.B), dim3(kStrataThreads), lds, p.stream,
-                                   a, (const int32_t*)dseq, p.n_seq, done, err);
+                if (p.flags & MF_FLAG_NO_COOP) {
+                    hipLaunchKernelGGL(efn, dim3((unsigned)p.B), dim3(kStrataThreads), lds,
+                                       p.stream, a, dseq, nseq, done, err);
+                } else {
+                    // cooperative: the runtime guarantees that all B workgroups
+                    // are resident at once (the neighbour waits need it) or
+                    // refuses the launch -- then one launch per stratum below
+                    void* kargs[] = {&a, &dseq, &nseq, &done, &err};
+                    const hipError_t ce = hipLaunchCooperativeKernel(
+                        reinterpret_cast<const void*>(efn), dim3((unsigned)p.B),
+                        dim3(kStrataThreads), kargs, (unsigned)lds, p.stream);
+                    if (ce != hipSuccess) {
+                        (void)hipGetLastError();
+                        persistent = false;
+                    }
+                }
             }
         }
         if (!persistent) {
+            const int64_t nq = p.n_items * (int64_t)p.k;
+            if (p.dq) {   // delta-out: keep the start values in D (see k_delta_swap)
+                MF_HIP_CHECK(hipMemcpyAsync(p.dq, p.Q, sizeof(T) * (size_t)nq,
+                                            hipMemcpyDeviceToDevice, p.stream));
+                if (KERN != MF_RBF)
+                    MF_HIP_CHECK(hipMemcpyAsync(p.dbi, p.bi, sizeof(T) * (size_t)p.n_items,
+                                                hipMemcpyDeviceToDevice, p.stream));
+            }
+            a.Dq = a.Dbi = nullptr;
             for (int32_t t = 0; t < p.n_seq; ++t) {
                 a.s = p.seq[t];
                 hipLaunchKernelGGL(kfn, dim3((unsigned)p.B), dim3(kStrataThreads), lds, p.stream,
                                    a);
+            }
+            if (p.dq) {
+                hipLaunchKernelGGL(k_delta_swap<T>, dim3(1024), dim3(kBlock), 0, p.stream,
+                                   static_cast<T*>(p.Q), static_cast<T*>(p.dq), nq);
+                if (KERN != MF_RBF)
+                    hipLaunchKernelGGL(k_delta_swap<T>, dim3(64), dim3(kBlock), 0, p.stream,
+                                       static_cast<T*>(p.bi), static_cast<T*>(p.dbi),
+                                       p.n_items);
             }
         }
         hipError_t le = hipGetLastError();

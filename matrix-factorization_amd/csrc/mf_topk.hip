@@ -4,7 +4,8 @@
 //
 // Stage 1 (k_topk_scores): one wave per (user, chunk of items); the user's
 //   factor row stays in registers, item rows stream from HBM/L2; each score
-//   becomes a 64-bit order-preserving key (0 = excluded, 1 = NaN).
+//   becomes a 64-bit order-preserving key (1 = NaN); k_topk_exclude then
+//   zeroes the keys of the excluded (user, item) pairs (CSR list).
 // Stage 2 (k_topk_select): one workgroup per user: 8-pass radix select of
 //   the amount-th key (LDS histograms), collect, bitonic sort in LDS by
 //   (score desc, item id asc).
@@ -32,7 +33,6 @@ template <typename T>
 struct TopkArgs {
     const int32_t* users;
     const T* P; const T* Q; const T* Bu; const T* Bi;
-    const uint8_t* exclude;
     int32_t n_items;
     int32_t k;
     Hyper<T> h;
@@ -84,9 +84,21 @@ __global__ __launch_bounds__(kBlock) void k_topk_scores(TopkArgs<T> A) {
             else if constexpr (KERN == MF_SIGMOID)
                 pred = A.h.a + A.h.c * ((T)1 / ((T)1 + dexp<T>(-(((A.h.mu + bu) + bi) + s))));
             else pred = A.h.a + A.h.c * dexp<T>((-A.h.gamma) * s);
-            const bool ex = A.exclude && A.exclude[(int64_t)qy * A.n_items + it];
-            keys[it] = ex ? 0ull : order_key((double)pred);
+            keys[it] = order_key((double)pred);
         }
+    }
+}
+
+// excluded (query, item) pairs: key 0, below every candidate.  One workgroup
+// per query walks its CSR list (ids outside [0, n_items) are ignored).
+__global__ __launch_bounds__(kBlock) void k_topk_exclude(uint64_t* __restrict__ keys,
+                                                         int32_t n_items,
+                                                         const int64_t* __restrict__ ptr,
+                                                         const int32_t* __restrict__ items) {
+    const int qy = blockIdx.x;
+    for (int64_t x = ptr[qy] + threadIdx.x; x < ptr[qy + 1]; x += kBlock) {
+        const int32_t it = items[x];
+        if (it >= 0 && it < n_items) keys[(int64_t)qy * n_items + it] = 0ull;
     }
 }
 
@@ -217,20 +229,23 @@ __global__ __launch_bounds__(kBlock) void k_topk_select(const uint64_t* __restri
 struct TopkLaunch {
     const int32_t* users; int32_t nq; double mu; const void* bu; const void* bi;
     const void* P; const void* Q; int32_t n_items; int32_t k; double gamma, lo, hi;
-    const uint8_t* exclude; int32_t amount; void* ws; int32_t* out_items; void* out_scores;
+    const int64_t* ex_ptr; const int32_t* ex_items; int32_t amount; void* ws; int32_t* out_items; void* out_scores;
     hipStream_t stream;
 
     template <typename T, int GS, int V, int KERN>
     int run() {
         TopkArgs<T> a;
         a.users = users; a.P = (const T*)P; a.Q = (const T*)Q;
-        a.Bu = (const T*)bu; a.Bi = (const T*)bi; a.exclude = exclude;
+        a.Bu = (const T*)bu; a.Bi = (const T*)bi;
         a.n_items = n_items; a.k = k; a.h = make_hyper<T>(mu, 0.0, 0.0, gamma, lo, hi);
         a.keys = (uint64_t*)ws;
         const int64_t waves = ((int64_t)n_items + kTopkItemsPerWave - 1) / kTopkItemsPerWave;
         const unsigned bx = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
         hipLaunchKernelGGL((k_topk_scores<T, GS, V, KERN>), dim3(bx, (unsigned)nq),
                            dim3(kBlock), 0, stream, a);
+        if (ex_ptr && ex_items)
+            hipLaunchKernelGGL(k_topk_exclude, dim3((unsigned)nq), dim3(kBlock), 0, stream,
+                               a.keys, n_items, ex_ptr, ex_items);
         int a2 = 1;
         while (a2 < amount) a2 <<= 1;
         hipLaunchKernelGGL(k_topk_select<T>, dim3((unsigned)nq), dim3(kBlock), 0, stream,
@@ -256,8 +271,8 @@ extern "C" int mf_topk(const int32_t* query_users, int32_t n_query, double globa
                        const void* user_biases, const void* item_biases,
                        const void* user_features, const void* item_features, int32_t n_items,
                        int32_t n_factors, int32_t kernel, int32_t dtype, double gamma,
-                       double min_rating, double max_rating, const uint8_t* exclude,
-                       int32_t amount, void* workspace, int32_t* out_items, void* out_scores,
+                       double min_rating, double max_rating, const int64_t* exclude_ptr,
+                       const int32_t* exclude_items, int32_t amount, void* workspace, int32_t* out_items, void* out_scores,
                        void* stream) {
     if (n_query < 0 || n_items < 0 || amount < 0 || amount > kTopkMaxAmount) {
         set_error("mf_topk: need 0 <= amount <= %d and non-negative sizes", kTopkMaxAmount);
@@ -274,7 +289,7 @@ extern "C" int mf_topk(const int32_t* query_users, int32_t n_query, double globa
         return MF_ERR_INVALID;
     }
     TopkLaunch L{query_users, n_query, global_mean, user_biases, item_biases, user_features,
-                 item_features, n_items, n_factors, gamma, min_rating, max_rating, exclude,
-                 amount, workspace, out_items, out_scores, (hipStream_t)stream};
+                 item_features, n_items, n_factors, gamma, min_rating, max_rating, exclude_ptr,
+                 exclude_items, amount, workspace, out_items, out_scores, (hipStream_t)stream};
     return dispatch(dtype, n_factors, kernel, L);
 }

@@ -22,6 +22,7 @@ MF_FLAG_NT_ITEM = 4
 MF_FLAG_XCD_CLAIM = 8
 MF_FLAG_PERSISTENT = 16
 MF_FLAG_DEEP_PIPE = 32
+MF_FLAG_NO_COOP = 64
 MF_ERR_CAPACITY = 3
 MF_DELTA_TAKE, MF_DELTA_APPLY = 0, 1
 KERNEL_CODES = {"linear": MF_LINEAR, "sigmoid": MF_SIGMOID, "rbf": MF_RBF}
@@ -54,6 +55,11 @@ SIGNATURES = {
         _I32, _I32, _F64, _F64, _F64, _F64, _F64,     # kernel dtype gamma lr reg min max
         _I32, _I32, _I32,                             # upd_u upd_i flags
         _P, ctypes.c_size_t, _P, _PD]),               # ws ws_bytes stream kernel_ms
+    "mf_sgd_epoch_strata_delta": (ctypes.c_int, [
+        _P, _P, _P, _I64, _I32, _P, _P, _P, _I32, _I32, _I32, _P, _I32, ctypes.c_uint32,
+        _F64, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F64, _F64, _F64, _F64, _F64,
+        _I32, _I32, _I32, _P, ctypes.c_size_t,
+        _P, _P, _P, _PD]),                            # item delta, bias delta, stream, ms
     "mf_strata_workspace_bytes": (ctypes.c_size_t, [_I32, _I32]),
     "mf_strata_status": (ctypes.c_int, [_P, _I32, _P]),
     "mf_strata_lds_bytes": (ctypes.c_size_t, [_I32, _I32, _I32, _I32]),
@@ -69,7 +75,7 @@ SIGNATURES = {
     "mf_topk_workspace_bytes": (ctypes.c_size_t, [_I32, _I32, _I32]),
     "mf_topk": (ctypes.c_int, [
         _P, _I32, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _F64, _F64,
-        _F64, _P, _I32, _P, _P, _P, _P]),
+        _F64, _P, _P, _I32, _P, _P, _P, _P]),
     "mf_bias_sgd_epoch": (ctypes.c_int, [
         _P, _P, _P, _I64, _P, _P, _I32, _P, _I32, _F64, _P, _P, _I32, _F64, _F64,
         _I32, _I32, _P]),
@@ -100,6 +106,7 @@ SIGNATURES = {
     "mf_pairs_duplicated": (ctypes.c_int, [_P, _P, _I64, _P]),
     "mf_factorize": (ctypes.c_int, [_P, _I64, _P, _P, _P]),
     "mf_gather": (ctypes.c_int, [_P, _I64, _I32, _P, _I64, _P]),
+    "mf_fingerprint": (ctypes.c_uint64, [_P, _I64]),
 }
 
 

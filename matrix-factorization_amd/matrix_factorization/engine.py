@@ -26,6 +26,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import warnings
 from typing import Optional, Sequence, Tuple
 
 import numpy as np
@@ -434,9 +435,11 @@ class SGDEngine:
 
     def epoch_strata(self, seq: Optional[np.ndarray], seed: int, lr: float, reg: float,
                      update_user: bool = True, update_item: bool = True, timing=False,
-                     persistent: Optional[bool] = None):
+                     persistent: Optional[bool] = None, delta=None):
         """Apply the strata listed in ``seq`` (a permutation of range(B) is
-        one epoch) with step rotation ``seed``."""
+        one epoch) with step rotation ``seed``.  ``delta`` = (dQ, db_i)
+        device tensors: delta-out form (mf_sgd_epoch_strata_delta) -- Q and
+        b_i keep their values, the epoch's item update goes to the deltas."""
         pl = self.strata
         if pl is None:
             raise RuntimeError("call prepare_strata() first")
@@ -444,23 +447,36 @@ class SGDEngine:
                else np.ascontiguousarray(seq, np.int32))
         ms = (ctypes.c_double * 2)() if timing else None
         if persistent is None:
-            persistent = self.strata_persistent
+            persistent = self.strata_persistent and os.environ.get("MF_STRATA_PERSISTENT") != "0"
         flags = _lib.MF_FLAG_PERSISTENT if persistent else 0
         if persistent and self._deep_pipe(pl):
             flags |= _lib.MF_FLAG_DEEP_PIPE
+        if os.environ.get("MF_STRATA_COOP") == "0":
+            flags |= _lib.MF_FLAG_NO_COOP
         wsb = int(_lib.load().mf_strata_workspace_bytes(pl.B, len(seq)))
-        if getattr(self, "_strata_ws", None) is None or self._strata_ws.numel() * 4 < wsb:
-            # zeroed once: the error flag is sticky until check_strata() raises
-            self._strata_ws = torch.zeros((wsb + 3) // 4, dtype=torch.int32, device=self.dev)
+        old = getattr(self, "_strata_ws", None)
+        if old is None or old.numel() * 4 < wsb:
+            # zeroed once: the error flag (int32 at index B) is sticky until
+            # check_strata() raises or clear_strata_error() resets it; a
+            # grown workspace carries a pending error over
+            ws = torch.zeros((wsb + 3) // 4, dtype=torch.int32, device=self.dev)
+            if old is not None:
+                ws[pl.B] = old[pl.B]
+            self._strata_ws = ws
+        args = (_tp(pl.d_u), _tp(pl.d_i), _tp(pl.d_r),
+                pl.n_positions, pl.B, _tp(pl.d_ubnd), _tp(pl.d_ibnd), _tp(pl.d_bstep),
+                pl.NS, pl.max_items, pl.max_users, _np(seq), len(seq),
+                int(seed) & 0xFFFFFFFF, self.global_mean, _tp(self.bu), _tp(self.bi),
+                _tp(self.P), _tp(self.Q), self.n_users, self.n_items, self.k,
+                self.kcode, self.dcode, self.gamma, float(lr), float(reg),
+                self.min_rating, self.max_rating, int(update_user), int(update_item),
+                flags, _tp(self._strata_ws), self._strata_ws.numel() * 4)
         with torch.cuda.device(self.dev):
-            _lib.call("mf_sgd_epoch_strata", _tp(pl.d_u), _tp(pl.d_i), _tp(pl.d_r),
-                      pl.n_positions, pl.B, _tp(pl.d_ubnd), _tp(pl.d_ibnd), _tp(pl.d_bstep),
-                      pl.NS, pl.max_items, pl.max_users, _np(seq), len(seq),
-                      int(seed) & 0xFFFFFFFF, self.global_mean, _tp(self.bu), _tp(self.bi),
-                      _tp(self.P), _tp(self.Q), self.n_users, self.n_items, self.k,
-                      self.kcode, self.dcode, self.gamma, float(lr), float(reg),
-                      self.min_rating, self.max_rating, int(update_user), int(update_item),
-                      flags, _tp(self._strata_ws), self._strata_ws.numel() * 4, self.stream, ms)
+            if delta is None:
+                _lib.call("mf_sgd_epoch_strata", *args, self.stream, ms)
+            else:
+                _lib.call("mf_sgd_epoch_strata_delta", *args, _tp(delta[0]), _tp(delta[1]),
+                          self.stream, ms)
         return (ms[0], int(ms[1])) if timing else None
 
     def check_strata(self) -> None:
@@ -471,6 +487,45 @@ class SGDEngine:
             return
         with torch.cuda.device(self.dev):
             _lib.call("mf_strata_status", _tp(ws), self.strata.B, self.stream)
+
+    def strata_failed(self) -> bool:
+        """Synchronise; True if a persistent sweep gave up waiting since the
+        error flag was last cleared (non-raising form of check_strata)."""
+        ws = getattr(self, "_strata_ws", None)
+        return ws is not None and int(ws[self.strata.B].item()) != 0
+
+    def clear_strata_error(self) -> None:
+        ws = getattr(self, "_strata_ws", None)
+        if ws is not None:
+            ws[self.strata.B] = 0
+
+    def snapshot_params(self):
+        """Device copies of (P, Q, b_u, b_i) (restore_params puts them back)."""
+        return tuple(None if t is None else t.clone() for t in (self.P, self.Q, self.bu, self.bi))
+
+    def restore_params(self, snap) -> None:
+        for t, s in zip((self.P, self.Q, self.bu, self.bi), snap):
+            if t is not None:
+                t.copy_(s)
+
+    def epoch_strata_checked(self, seq, seed, lr, reg, update_user=True, update_item=True):
+        """One strata epoch that cannot leave invalid parameters behind: the
+        persistent sweep runs from a device snapshot of the parameters; if a
+        workgroup gave up waiting for its neighbour (another process holding
+        CUs, say), the snapshot is restored and the same epoch -- same
+        strata, same rotation, hence the same sequential order -- is re-run
+        as one launch per stratum.  Returns True if the fallback ran."""
+        if not self.strata_persistent:
+            self.epoch_strata(seq, seed, lr, reg, update_user, update_item)
+            return False
+        snap = self.snapshot_params()
+        self.epoch_strata(seq, seed, lr, reg, update_user, update_item)
+        if not self.strata_failed():
+            return False
+        self.restore_params(snap)
+        self.clear_strata_error()
+        self.epoch_strata(seq, seed, lr, reg, update_user, update_item, persistent=False)
+        return True
 
     def epoch_exact(self, order: np.ndarray, lr: float, reg: float,
                     update_user: bool = True, update_item: bool = True,
@@ -579,29 +634,54 @@ class SGDEngine:
                           self.max_rating, int(bound), _tp(out), self.stream)
         return out.cpu().numpy().astype(np.float64)
 
-    def topk(self, users: np.ndarray, amount: int,
-             exclude: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
-        """Best ``amount`` items per internal user id: (item ids, scores)."""
+    # score keys of one top-k launch: n_query * n_items * 8 B; users beyond
+    # this budget go in further launches
+    topk_ws_budget = 1 << 30
+
+    def topk(self, users: np.ndarray, amount: int, ex_ptr: Optional[np.ndarray] = None,
+             ex_items: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """Best ``amount`` items per internal user id: (item ids, scores).
+
+        ``ex_ptr`` / ``ex_items``: optional CSR exclusions (query q skips
+        items ex_items[ex_ptr[q]:ex_ptr[q+1]]).  Users are processed in
+        chunks whose score workspace fits ``topk_ws_budget``."""
         if self.bias_only:
             raise NotImplementedError("top-k is implemented for factor models")
+        users = np.ascontiguousarray(users, np.int32)
         nq = len(users)
-        items = torch.empty((nq, amount), dtype=torch.int32, device=self.dev)
-        scores = torch.empty((nq, amount), dtype=self.tdt, device=self.dev)
+        items_out = np.full((nq, amount), -1, np.int32)
+        scores_out = np.full((nq, amount), np.nan, np.float64)
         if nq == 0 or amount == 0:
-            return items.cpu().numpy(), scores.cpu().numpy().astype(np.float64)
-        ud = torch.from_numpy(np.ascontiguousarray(users, np.int32)).to(self.dev)
-        ex = None
-        if exclude is not None:
-            ex = torch.from_numpy(np.ascontiguousarray(exclude, np.uint8)).to(self.dev)
-        wsb = _lib.load().mf_topk_workspace_bytes(nq, self.n_items, amount)
+            return items_out, scores_out
+        if ex_ptr is not None:
+            ex_ptr = np.ascontiguousarray(ex_ptr, np.int64)
+            ex_items = np.ascontiguousarray(ex_items, np.int32)
+            if len(ex_ptr) != nq + 1:
+                raise ValueError("ex_ptr needs n_query + 1 offsets")
+        lib = _lib.load()
+        chunk = int(max(1, min(65535, self.topk_ws_budget // max(8 * self.n_items, 1), nq)))
+        wsb = lib.mf_topk_workspace_bytes(chunk, self.n_items, amount)
         ws = torch.empty(max(wsb, 8), dtype=torch.uint8, device=self.dev)
-        with torch.cuda.device(self.dev):
-            _lib.call("mf_topk", _tp(ud), nq, self.global_mean, _tp(self.bu),
-                      _tp(self.bi), _tp(self.P), _tp(self.Q), self.n_items, self.k,
-                      self.kcode, self.dcode, self.gamma, self.min_rating,
-                      self.max_rating, _tp(ex), amount, _tp(ws), _tp(items),
-                      _tp(scores), self.stream)
-        return items.cpu().numpy(), scores.cpu().numpy().astype(np.float64)
+        d_items = torch.empty((chunk, amount), dtype=torch.int32, device=self.dev)
+        d_scores = torch.empty((chunk, amount), dtype=self.tdt, device=self.dev)
+        for q0 in range(0, nq, chunk):
+            q1 = min(nq, q0 + chunk)
+            ud = torch.from_numpy(users[q0:q1]).to(self.dev)
+            dp = di = None
+            if ex_ptr is not None:
+                lo, hi = int(ex_ptr[q0]), int(ex_ptr[q1])
+                dp = torch.from_numpy(ex_ptr[q0:q1 + 1] - lo).to(self.dev)
+                di = torch.from_numpy(ex_items[lo:hi] if hi > lo else
+                                      np.zeros(1, np.int32)).to(self.dev)
+            with torch.cuda.device(self.dev):
+                _lib.call("mf_topk", _tp(ud), q1 - q0, self.global_mean, _tp(self.bu),
+                          _tp(self.bi), _tp(self.P), _tp(self.Q), self.n_items, self.k,
+                          self.kcode, self.dcode, self.gamma, self.min_rating,
+                          self.max_rating, _tp(dp), _tp(di), amount, _tp(ws), _tp(d_items),
+                          _tp(d_scores), self.stream)
+            items_out[q0:q1] = d_items[: q1 - q0].cpu().numpy()
+            scores_out[q0:q1] = d_scores[: q1 - q0].cpu().numpy()
+        return items_out, scores_out
 
 
 class BiasALS:
@@ -719,7 +799,10 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
         else:
             seq = np.random.permutation(nb).astype(np.int32)
             seed = int(np.random.randint(0, 2**31 - 1))
-            engine.epoch_strata(seq, seed, lr, reg, update_user, update_item)
+            if engine.epoch_strata_checked(seq, seed, lr, reg, update_user, update_item):
+                warnings.warn(f"epoch {epoch + 1}: the persistent strata sweep could not "
+                              "complete (workgroups not co-resident); re-ran the epoch as "
+                              "one launch per stratum", RuntimeWarning, stacklevel=2)
         engine.sse_async(epoch)
         if verbose == 1:
             rmse = engine.rmse_values(epoch + 1)[epoch]
@@ -727,8 +810,6 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
             print("Epoch ", epoch + 1, "/", n_epochs, " -  train_rmse:", rmse)
         if on_epoch is not None:
             on_epoch(epoch)
-    if schedule == "strata":
-        engine.check_strata()
     if verbose != 1:
         train_rmse = engine.rmse_values(n_epochs)
     return train_rmse

@@ -15,6 +15,13 @@ Three keyword arguments are new and default to the reference's behaviour:
               blocks, item slabs resident in LDS; mf_strata.hpp), also a
               valid sequential order per epoch -- the throughput setting.
 ``device``    HIP device ("cuda", "cuda:1", ...); None = current device.
+``distributed`` False (default) or True: process-group mode.  When
+              torch.distributed is initialised with world_size > 1, every
+              rank calls ``fit`` with the same data and the same NumPy RNG
+              state; users are sharded across the ranks (one GPU each,
+              RCCL all-reduce of the item-row deltas once per epoch,
+              distributed.fit_sharded) and every rank ends with the full
+              model.  Needs schedule "strata" or "colored".
 """
 
 from __future__ import annotations
@@ -24,8 +31,43 @@ from typing import Union
 import numpy as np
 import pandas as pd
 
+from . import _lib
+from .distributed import fit_sharded, world_info
 from .engine import SGDEngine, canonical_dtype, fit_epochs
 from .recommender_base import RecommenderBase
+
+
+def _fingerprint(a) -> tuple:
+    a = np.ascontiguousarray(a)
+    return (a.shape, a.dtype.str, int(_lib.load().mf_fingerprint(a.ctypes.data, a.nbytes)))
+
+
+def _warn_if_no_device() -> None:
+    """Unpickling on a host without a usable GPU stack: the model loads (its
+    NumPy attributes are complete) but cannot score.  Say so at load time:
+    a serving wrapper that turns predict()'s exception into a default score
+    (the reference's project_template/app/api.py:49-52 returns zeros) would
+    otherwise hide it."""
+    import warnings
+
+    reason = None
+    try:
+        import torch
+
+        if not torch.cuda.is_available():
+            reason = "no HIP device is visible"
+    except Exception as e:  # pragma: no cover - torch is a dependency
+        reason = f"torch is unavailable ({e})"
+    if reason is None:
+        try:
+            _lib.load()
+        except _lib.MFLibraryError as e:
+            reason = str(e)
+    if reason is not None:
+        warnings.warn(f"KernelMF loaded, but {reason}: predict() and recommend() will raise "
+                      "MFLibraryError on this host (they run on an AMD Instinct GPU "
+                      "through libmf_hip.so); the parameters are plain NumPy attributes",
+                      RuntimeWarning, stacklevel=3)
 
 
 class KernelMF(RecommenderBase):
@@ -43,7 +85,7 @@ class KernelMF(RecommenderBase):
                  reg: float = 1, lr: float = 0.01, init_mean: float = 0,
                  init_sd: float = 0.1, min_rating: int = 0, max_rating: int = 5,
                  verbose: int = 1, dtype: str = "float64",
-                 schedule: str = "exact", device=None):
+                 schedule: str = "exact", device=None, distributed: bool = False):
         if kernel not in ("linear", "sigmoid", "rbf"):
             raise ValueError("Kernel must be one of linear, sigmoid, or rbf")
         if schedule not in ("exact", "colored", "strata"):
@@ -62,6 +104,7 @@ class KernelMF(RecommenderBase):
         self.dtype = dtype
         self.schedule = schedule
         self.device = device
+        self.distributed = distributed
 
     # ----------------------------------------------------- device state
     def _make_engine(self, X: pd.DataFrame) -> SGDEngine:
@@ -78,17 +121,26 @@ class KernelMF(RecommenderBase):
         P, Q, bu, bi = eng.params_numpy()
         self.user_features, self.item_features = P, Q
         self.user_biases, self.item_biases = bu, bi
-        self._param_ids = self._ids()
+        self._pred_key = self._param_key()
 
-    def _ids(self):
-        return tuple(id(a) for a in (self.user_features, self.item_features,
-                                     self.user_biases, self.item_biases))
+    def _param_key(self):
+        """What the device copies were made from: the attribute arrays (by
+        identity) and a fingerprint of their bytes, so replaced arrays and
+        in-place edits (``model.item_features[3] = ...``, update_users'
+        row resets) are both seen -- the reference predicts from the live
+        arrays (kernel_matrix_factorization.py:148-160)."""
+        arrs = (self.user_features, self.item_features, self.user_biases, self.item_biases)
+        return arrs, tuple(_fingerprint(a) for a in arrs)
 
     def _predictor(self) -> SGDEngine:
-        """Engine holding the current parameters (re-uploaded when the
-        attribute arrays were replaced, e.g. after unpickling)."""
+        """Engine holding the current parameters, re-uploaded whenever the
+        attribute arrays were replaced or edited since the last upload."""
         eng = getattr(self, "_pred_engine", None)
-        if eng is None or getattr(self, "_param_ids", None) != self._ids():
+        key = self._param_key()
+        old = getattr(self, "_pred_key", None)
+        same = (old is not None and all(a is b for a, b in zip(old[0], key[0]))
+                and old[1] == key[1])
+        if eng is None or not same:
             eng = SGDEngine(np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0),
                             len(self.user_features), len(self.item_features),
                             self.n_factors, self.kernel, self.dtype, self.device,
@@ -97,15 +149,22 @@ class KernelMF(RecommenderBase):
             eng.load_params(self.user_features, self.item_features,
                             self.user_biases, self.item_biases)
             self._pred_engine = eng
-            self._param_ids = self._ids()
+            self._pred_key = key
         return eng
 
     def __getstate__(self):
-        # pickles carry plain NumPy state only (loadable without a GPU)
+        # pickles carry plain NumPy state only: they load on a host without a
+        # GPU or libmf_hip.so (attributes, get_params, recommend's id maps);
+        # predict / recommend need a HIP device (see __setstate__)
         state = self.__dict__.copy()
         state.pop("_pred_engine", None)
+        state.pop("_pred_key", None)
         state.pop("_param_ids", None)
         return state
+
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        _warn_if_no_device()
 
     # ------------------------------------------------------------ API
     def fit(self, X: pd.DataFrame, y: pd.Series):
@@ -119,6 +178,22 @@ class KernelMF(RecommenderBase):
                                               (self.n_users, self.n_factors))
         self.item_features = np.random.normal(self.init_mean, self.init_sd,
                                               (self.n_items, self.n_factors))
+        if self.distributed and world_info()[0] > 1:
+            n = len(X)
+            P, Q, bu, bi, rmse, _ = fit_sharded(
+                X["user_id"].to_numpy(np.int32), X["item_id"].to_numpy(np.int32),
+                X["rating"].to_numpy(np.float64), self.n_users, self.n_items,
+                self.user_features, self.item_features, self.user_biases, self.item_biases,
+                self.n_epochs, self.kernel, self.n_factors, self.dtype, self.device, self.gamma,
+                self.min_rating, self.max_rating, self.global_mean, self.lr, self.reg,
+                self.schedule, verbose=self.verbose) if n else (
+                self.user_features, self.item_features, self.user_biases, self.item_biases,
+                [float("nan")] * self.n_epochs, None)
+            self.user_features, self.item_features = P, Q
+            self.user_biases, self.item_biases = bu, bi
+            self.train_rmse = rmse
+            self._pred_engine = None
+            return self
         eng = self._make_engine(X)
         eng.load_params(self.user_features, self.item_features,
                         self.user_biases, self.item_biases)
@@ -166,32 +241,46 @@ class KernelMF(RecommenderBase):
 
     def recommend_batch(self, users, amount: int = 10, exclude_known=None,
                         bound_ratings: bool = True) -> pd.DataFrame:
-        """Top ``amount`` items for many users in one GPU pass (mf_topk).
+        """Top ``amount`` items for many users on the GPU (mf_topk) -- the
+        batched form of ``recommend`` (recommender_base.py:214-271).
 
         ``exclude_known``: optional DataFrame[user_id, item_id] of pairs to
-        skip.  Ties rank the lower internal item id first (recommend() keeps
-        pandas' order instead).  Returns DataFrame[user_id, item_id,
+        skip (recommend's ``items_known`` per user), passed to the device as
+        a CSR list.  Scores are recommend()'s (the unbounded prediction);
+        equal scores rank the lower internal item id first -- the order a
+        stable sort gives; the reference's ``sort_values`` default quicksort
+        leaves tie order unspecified.  Users go in chunks (engine
+        ``topk_ws_budget``).  Returns DataFrame[user_id, item_id,
         rating_pred] ordered by user then rank."""
         users = list(users)
         uid = self._remap(pd.Series(users, dtype=object), self.user_id_map)
-        exclude = None
+        ex_ptr = ex_items = None
         if exclude_known is not None and len(exclude_known):
-            exclude = np.zeros((len(users), self.n_items), np.uint8)
-            pos = {u: n for n, u in enumerate(users)}
-            ex_u = exclude_known["user_id"].map(pos)
-            ex_i = self._remap(exclude_known["item_id"], self.item_id_map)
-            ok = ex_u.notna().to_numpy() & (ex_i >= 0)
-            exclude[ex_u[ok].astype(np.int64).to_numpy(), ex_i[ok]] = 1
+            pos = pd.Series(np.arange(len(users)), index=pd.Index(users, dtype=object))
+            pos = pos[~pos.index.duplicated(keep="first")]
+            q = exclude_known["user_id"].map(pos)
+            it = self._remap(exclude_known["item_id"], self.item_id_map)
+            ok = q.notna().to_numpy() & (it >= 0)
+            qv = q[ok].to_numpy().astype(np.int64)
+            iv = it[ok].astype(np.int32)
+            # duplicate users in `users` share the first position's list
+            first = pos.reindex(pd.Index(users, dtype=object)).to_numpy().astype(np.int64)
+            order = np.argsort(qv, kind="stable")
+            qv, iv = qv[order], iv[order]
+            cnt = np.bincount(qv, minlength=len(users)).astype(np.int64)
+            start = np.concatenate([[0], np.cumsum(cnt)])
+            per = [iv[start[f]:start[f + 1]] for f in first]
+            ex_ptr = np.concatenate([[0], np.cumsum([len(x) for x in per])]).astype(np.int64)
+            ex_items = (np.concatenate(per) if len(per) else np.zeros(0)).astype(np.int32)
         amount = min(amount, self.n_items)
-        items, scores = self._predictor().topk(uid, amount, exclude)
+        items, scores = self._predictor().topk(uid, amount, ex_ptr, ex_items)
         inv = np.asarray(list(self.item_id_map.keys()), dtype=object)
-        rows_u, rows_i, rows_s = [], [], []
-        for q, user in enumerate(users):
-            valid = items[q] >= 0
-            rows_u += [user] * int(valid.sum())
-            rows_i += list(inv[items[q][valid]])
-            rows_s += list(scores[q][valid])
-        out = pd.DataFrame({"user_id": rows_u, "item_id": rows_i, "rating_pred": rows_s})
+        valid = items >= 0
+        out = pd.DataFrame({
+            "user_id": np.repeat(np.asarray(users, dtype=object), valid.sum(axis=1)),
+            "item_id": inv[items[valid]],
+            "rating_pred": scores[valid],
+        })
         if bound_ratings:
             out["rating_pred"] = out["rating_pred"].clip(lower=self.min_rating,
                                                          upper=self.max_rating)

@@ -83,16 +83,23 @@ class CpuEngine:
         self.strata = StrataPlan(B, ns, ub, ib, bstep, sched)
         return self.strata
 
-    def epoch_strata(self, seq, seed, lr, reg, timing=False):
+    def epoch_strata(self, seq, seed, lr, reg, update_user=True, update_item=True,
+                     timing=False, delta=None):
         order = self.strata.serial_order(seq, seed)
+        Q0, bi0 = self.Q.clone(), self.bi.clone()
         oracle.sgd_pass(self.u_host, self.i_host, self.r_host, self.global_mean,
                         self.bu.numpy(), self.bi.numpy(), self.P.numpy(), self.Q.numpy(),
                         lr=lr, reg=reg, order=order)
+        if delta is not None:          # delta-out form: replica untouched
+            delta[0].copy_(self.Q - Q0)
+            delta[1].copy_(self.bi - bi0)
+            self.Q.copy_(Q0)
+            self.bi.copy_(bi0)
 
     def check_strata(self):
         pass
 
-    def epoch_colored(self, seq, lr, reg, timing=False):
+    def epoch_colored(self, seq, lr, reg, update_user=True, update_item=True, timing=False):
         order = np.concatenate([np.arange(self.colored[b], self.colored[b + 1])
                                 for b in seq]).astype(np.int64)
         Q = self.Q.numpy()
@@ -113,9 +120,9 @@ def _exchange_cls():
         def _delta(self, mode):                       # mf_replica_delta on CPU
             from matrix_factorization import _lib
             if mode == _lib.MF_DELTA_TAKE:
-                self.flat.sub_(self.snap)
+                self.flat.sub_(self.delta)
             else:
-                self.flat.add_(self.snap)
+                self.flat.add_(self.delta)
 
     return CpuExchange
 
@@ -225,4 +232,110 @@ def test_two_rank_gloo_exchange_matches_simulation(tmp_path, schedule):
     for k in range(world):
         assert np.max(np.abs(res[k]["P"] - engs[k].P.numpy())) < 1e-12
     assert np.max(np.abs(res[0]["rmse"] - rmse)) < 1e-12
+    assert rmse[-1] < rmse[0]
+
+
+# ------------------------------------------------ the estimator surface
+def _cpu_engine_factory(u, i, r, n_users, n_items, k, kernel, dtype, device, gamma=0.0,
+                        min_rating=0.0, max_rating=5.0, global_mean=0.0):
+    return CpuEngine(u, i, r.astype(np.float64), n_users, n_items, k, global_mean)
+
+
+FIT_HP = dict(n_factors=K, n_epochs=EPOCHS, lr=LR, reg=REG, min_rating=1, max_rating=5,
+              verbose=0, schedule="strata")
+
+
+def _frame():
+    import pandas as pd
+
+    u, i, r, _, _ = _data()
+    # external ids differ from internal ones (first appearance after the shuffle)
+    return pd.DataFrame({"user_id": u * 7 + 3, "item_id": i * 5 + 1}), pd.Series(r)
+
+
+def _fit_rank(rank, world, port, out_dir):
+    """KernelMF(distributed=True).fit on every rank: the product's sharding,
+    per-epoch draws, delta all-reduce and final gathers; the device sweeps
+    are the CPU test double."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import matrix_factorization as mf
+    import matrix_factorization.distributed as D
+
+    D.SGDEngine = _cpu_engine_factory
+    D.ReplicaExchange = _exchange_cls()
+    X, y = _frame()
+    np.random.seed(SEED)
+    m = mf.KernelMF(distributed=True, **FIT_HP).fit(X, y)
+    np.savez(os.path.join(out_dir, f"fit{rank}.npz"), P=m.user_features, Q=m.item_features,
+             bu=m.user_biases, bi=m.item_biases, rmse=np.asarray(m.train_rmse),
+             uids=np.asarray(list(m.user_id_map)), iids=np.asarray(list(m.item_id_map)))
+    dist.destroy_process_group()
+
+
+def _simulate_fit(world):
+    """Single-process restatement of KernelMF(distributed=True).fit: the
+    reference's draws (sample, normal(P), normal(Q)), then per epoch one
+    np.random.randint shared by all ranks, rank r's strata drawn from
+    RandomState([draw, r]); replica = start + sum of the rank deltas."""
+    import matrix_factorization as mf
+    from matrix_factorization.distributed import local_shard, shard_users
+
+    X, y = _frame()
+    np.random.seed(SEED)
+    m = mf.KernelMF(**FIT_HP)
+    Xp = m._preprocess_data(X=X, y=y, type="fit")
+    mu = Xp["rating"].mean()
+    P = np.random.normal(0, 0.1, (m.n_users, K))
+    Q = np.random.normal(0, 0.1, (m.n_items, K))
+    u = Xp["user_id"].to_numpy(np.int32)
+    i = Xp["item_id"].to_numpy(np.int32)
+    r = Xp["rating"].to_numpy(np.float64)
+    bounds = shard_users(u, m.n_users, world)
+    engs = []
+    for rank in range(world):
+        lu, li, lr_ = local_shard(u, i, r, bounds, rank)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        e = CpuEngine(lu, li, lr_, hi - lo, m.n_items, K, mu)
+        e.load_params(P=P[lo:hi], bu=np.zeros(hi - lo), Q=Q, bi=np.zeros(m.n_items))
+        e.prepare_strata()
+        engs.append(e)
+    bi = np.zeros(m.n_items)
+    sse = np.zeros(EPOCHS)
+    for ep in range(EPOCHS):
+        draw = int(np.random.randint(0, 2**31 - 1))
+        dQ, dbi = np.zeros_like(Q), np.zeros_like(bi)
+        for rank, e in enumerate(engs):
+            e.Q = torch.as_tensor(Q.copy())
+            e.bi = torch.as_tensor(bi.copy())
+            rs = np.random.RandomState([draw, rank])
+            seq = rs.permutation(e.strata.B)
+            e.epoch_strata(seq, int(rs.randint(0, 2**31 - 1)), LR, REG)
+            dQ += e.Q.numpy() - Q
+            dbi += e.bi.numpy() - bi
+        Q, bi = Q + dQ, bi + dbi
+        for e in engs:
+            e.Q = torch.as_tensor(Q.copy())
+            e.bi = torch.as_tensor(bi.copy())
+            e.sse_async(ep)
+            sse[ep] += float(e.sse_buf[ep])
+    P = np.concatenate([e.P.numpy() for e in engs])
+    bu = np.concatenate([e.bu.numpy() for e in engs])
+    return P, Q, bu, bi, np.sqrt(sse / len(u))
+
+
+@pytest.mark.timeout(300)
+def test_kernelmf_distributed_fit_two_ranks(tmp_path):
+    """The estimator's process-group mode (row 8(e) through fit()): both
+    ranks end with the same full model, equal to the restated algorithm."""
+    world = 2
+    mp.start_processes(_fit_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    res = [dict(np.load(tmp_path / f"fit{k}.npz")) for k in range(world)]
+    for key in ("P", "Q", "bu", "bi", "rmse", "uids", "iids"):
+        assert np.array_equal(res[0][key], res[1][key]), key
+    P, Q, bu, bi, rmse = _simulate_fit(world)
+    for key, ref in (("P", P), ("Q", Q), ("bu", bu), ("bi", bi), ("rmse", rmse)):
+        assert np.max(np.abs(res[0][key] - ref)) < 1e-12, key
     assert rmse[-1] < rmse[0]

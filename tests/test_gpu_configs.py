@@ -1,0 +1,141 @@
+"""GPU runs at the shapes BASELINE.json names (configs[1], [2], [4]), through
+the C ABI, against the FP64 oracle where the oracle finishes in seconds and
+through size-independent properties where it does not.
+
+  C2  100K x 10K, 5M ratings, sigmoid rank 32 (kernels.py:183-262):
+      two strata epochs in FP32 vs the oracle run in the GPU's serialised
+      order -- train RMSE |diff| <= 1e-5 (the north-star bar); one FP64
+      epoch -- parameters max |diff| <= 1e-11 * max(1, |value|).
+  C3  1M x 100K, 100M ratings, linear rank 64: the persistent epoch (one
+      launch, item slabs resident) is bit-identical to one launch per
+      stratum; train RMSE finite and falling over two epochs.  (The full-
+      epoch C3 comparison with the oracle, in the GPU's order and in the
+      reference's shuffle order, is bench.py's parity leg: ~1 min of CPU.)
+  C5  1M x 100K, 100M ratings, ALS rank 128: the user half-sweep of the
+      first 10K users vs oracle.als_half_sweep -- parameters max relative
+      diff <= 2e-4 (f32 MFMA Gramian + f32 solve vs f64).
+"""
+
+import os
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _synth(nu, ni, nnz):
+    sys.path.insert(0, ROOT)
+    from bench import synth       # the bench's generator: same data as the bench lines
+
+    return synth(nu, ni, nnz)
+
+
+@pytest.fixture(scope="module")
+def c3_data():
+    return _synth(1_000_000, 100_000, 100_000_000)
+
+
+def _engine(u, i, r, nu, ni, k, kernel, dtype):
+    from matrix_factorization.engine import SGDEngine
+
+    return SGDEngine(u, i, r, nu, ni, k, kernel, dtype, "cuda:0", gamma=1.0 / k,
+                     min_rating=1.0, max_rating=5.0,
+                     global_mean=float(np.mean(r, dtype=np.float64)))
+
+
+def _init(nu, ni, k, dtype, seed=7):
+    rs = np.random.RandomState(seed)
+    return rs.normal(0, 0.1, (nu, k)).astype(dtype), rs.normal(0, 0.1, (ni, k)).astype(dtype)
+
+
+def test_c2_shape_strata_vs_oracle():
+    import oracle
+
+    nu, ni, nnz, k = 100_000, 10_000, 5_000_000, 32
+    u, i, r = _synth(nu, ni, nnz)
+    hyp = dict(kernel="sigmoid", gamma=1.0 / k, min_rating=1.0, max_rating=5.0)
+    rs = np.random.RandomState(3)
+    for dtype, epochs in (("float32", 2), ("float64", 1)):
+        P0, Q0 = _init(nu, ni, k, dtype)
+        eng = _engine(u, i, r, nu, ni, k, "sigmoid", dtype)
+        plan = eng.prepare_strata()
+        eng.load_params(P0, Q0, np.zeros(nu), np.zeros(ni))
+        mu = eng.global_mean
+        P, Q = P0.astype(np.float64), Q0.astype(np.float64)
+        bu, bi = np.zeros(nu), np.zeros(ni)
+        r64 = eng.r_host.astype(np.float64)
+        for ep in range(epochs):
+            seq = rs.permutation(plan.B).astype(np.int32)
+            seed = int(rs.randint(0, 2**31 - 1))
+            eng.epoch_strata(seq, seed, lr=0.01, reg=0.02)
+            eng.sse_async(ep)
+            oracle.sgd_pass(eng.u_host, eng.i_host, r64, mu, bu, bi, P, Q, lr=0.01, reg=0.02,
+                            order=plan.serial_order(seq, seed), **hyp)
+        eng.check_strata()
+        rm_o = oracle.rmse(eng.u_host, eng.i_host, r64, mu, bu, bi, P, Q, **hyp)
+        rm_g = eng.rmse_values(epochs)[-1]
+        if dtype == "float32":
+            assert abs(rm_g - rm_o) <= 1e-5, (rm_g, rm_o)
+        else:
+            Pg, Qg, bug, big = eng.params_numpy()
+            for a, b in ((Pg, P), (Qg, Q), (bug, bu), (big, bi)):
+                err = float(np.max(np.abs(a - b)))
+                assert err <= 1e-11 * max(1.0, float(np.max(np.abs(b)))), err
+            assert abs(rm_g - rm_o) <= 1e-12
+        del eng
+
+
+def test_c3_shape_persistent_equals_per_stratum(c3_data):
+    import torch
+
+    u, i, r = c3_data
+    nu, ni, k = 1_000_000, 100_000, 64
+    P0, Q0 = _init(nu, ni, k, np.float32)
+    eng = _engine(u, i, r, nu, ni, k, "linear", "float32")
+    plan = eng.prepare_strata()
+    assert plan.B == 256
+    rs = np.random.RandomState(5)
+    seqs = [rs.permutation(plan.B).astype(np.int32) for _ in range(2)]
+    seeds = [int(x) for x in rs.randint(0, 2**31 - 1, 2)]
+    out = []
+    for persistent in (False, True):
+        eng.load_params(P0, Q0, np.zeros(nu), np.zeros(ni))
+        _, n_launch = eng.epoch_strata(seqs[0], seeds[0], 0.01, 0.02, timing=True,
+                                       persistent=persistent)
+        assert n_launch == (1 if persistent else plan.B)
+        eng.check_strata()
+        out.append([t.clone() for t in (eng.P, eng.Q, eng.bu, eng.bi)])
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+    del out
+    eng.sse_async(0)
+    eng.epoch_strata(seqs[1], seeds[1], 0.01, 0.02)
+    eng.sse_async(1)
+    eng.check_strata()
+    rm = eng.rmse_values(2)
+    assert all(np.isfinite(rm)) and rm[1] < rm[0] < 1.2, rm
+
+
+def test_c5_shape_als_user_half_sweep(c3_data):
+    import oracle
+    from matrix_factorization.engine import FactorALS
+
+    u, i, r = c3_data
+    nu, ni, k, reg = 1_000_000, 100_000, 128, 1.0
+    P0, Q0 = _init(nu, ni, k, np.float32)
+    eng = _engine(u, i, r, nu, ni, k, "linear", "float32")
+    eng.load_params(P0, Q0, np.zeros(nu), np.zeros(ni))
+    als = FactorALS(eng)
+    als.sweep_users(reg)
+    Pg, _, bug, _ = eng.params_numpy()
+    n_s = 10_000
+    sel = u < n_s
+    mu = np.float32(eng.global_mean)
+    bo, Po = oracle.als_half_sweep(u[sel], i[sel], r[sel], mu, np.zeros(ni), Q0, n_s, reg)
+    rel = np.abs(Pg[:n_s] - Po) / np.maximum(1.0, np.abs(Po))
+    assert float(rel.max()) <= 2e-4, float(rel.max())
+    assert float(np.max(np.abs(bug[:n_s] - bo))) <= 2e-4

@@ -75,12 +75,23 @@ def test_kernelmf_matches_reference(mf, name, capsys):
     assert m.predictions_possible == d["pred_possible"].tolist()
     _close(m.predict(T, bound_ratings=False), d["pred_unbound"])
     df = X.assign(rating=y)
+    excl = []
     for j, user in enumerate(d["rec_users"]):
         known = df.loc[df.user_id == user, "item_id"].to_numpy()
         known = known[: len(known) // 2] if j % 2 == 0 else None
         rec = m.recommend(user=user, amount=10, items_known=known)
         assert rec["item_id"].tolist() == d["rec_items"][j].tolist()
         _close(rec["rating_pred"].to_numpy(), d["rec_pred"][j])
+        if known is not None:
+            excl.append(pd.DataFrame({"user_id": user, "item_id": known}))
+    # the batched GPU top-k (mf_topk, row f1) against the same golden lists:
+    # all rec_users in one call, items_known passed as the exclusion CSR
+    users = list(d["rec_users"])
+    got = m.recommend_batch(users, amount=10, exclude_known=pd.concat(excl))
+    for j, user in enumerate(users):
+        g = got[got.user_id == user]
+        assert g["item_id"].tolist() == d["rec_items"][j].tolist()
+        _close(g["rating_pred"].to_numpy(), d["rec_pred"][j])
 
 
 def test_update_users_matches_reference(mf):
@@ -214,20 +225,64 @@ def test_predict_edge_cases(mf):
     assert m.predictions_possible == [False, False]
 
 
-def test_topk_matches_host_ranking(mf):
+def test_topk_ties_and_chunking(mf):
+    """Equal scores: recommend_batch ranks the lower internal item id first,
+    the order a stable descending sort of recommend()'s candidate list gives
+    (the reference's quicksort leaves tie order unspecified,
+    recommender_base.py:259).  Several chunks of users give the same result
+    as one launch; duplicate query users are answered twice."""
     d = load_golden("c1_linear")
     hp = golden_hp(d)
+    hp.update(n_epochs=2, verbose=0)
     X, y = _frame(d)
     np.random.seed(int(d["seed"]))
-    hp["n_epochs"] = 2
     m = mf.KernelMF(**hp).fit(X, y)
-    users = list(d["rec_users"])
-    got = m.recommend_batch(users, amount=10, bound_ratings=False)
+    Q, bi = m.item_features.copy(), m.item_biases.copy()
+    # five items share the parameters of item 0: exact ties
+    for t in (7, 3, 900, 1500, 42):
+        Q[t] = Q[0]
+        bi[t] = bi[0]
+    m.item_features, m.item_biases = Q, bi
+    inv = list(m.item_id_map.keys())
+    users = list(d["rec_users"]) + [d["rec_users"][0]]
+    one = m.recommend_batch(users, amount=40, bound_ratings=False)
+    eng = m._predictor()
+    eng.topk_ws_budget = 8 * m.n_items * 2          # two users per launch
+    try:
+        many = m.recommend_batch(users, amount=40, bound_ratings=False)
+    finally:
+        eng.topk_ws_budget = type(eng).topk_ws_budget
+    pd.testing.assert_frame_equal(one, many)
     for user in users:
-        ref = m.recommend(user=user, amount=10, bound_ratings=False)
-        g = got[got.user_id == user]
-        assert g["item_id"].tolist() == ref["item_id"].tolist()
-        _close(g["rating_pred"].to_numpy(), ref["rating_pred"].to_numpy(), 1e-14)
+        cand = pd.DataFrame({"user_id": user, "item_id": inv})
+        cand["rating_pred"] = m.predict(cand, bound_ratings=False)
+        ref = cand.sort_values("rating_pred", ascending=False, kind="stable").head(40)
+        g = one[one.user_id == user]
+        assert len(g) == 40 * users.count(user)
+        assert g["item_id"].tolist()[:40] == ref["item_id"].tolist()
+        assert np.array_equal(g["rating_pred"].to_numpy()[:40], ref["rating_pred"].to_numpy())
+
+
+def test_predict_sees_in_place_edits(mf):
+    """The device copy follows the NumPy attributes, in-place edits included
+    (the reference predicts from the live arrays, :148-160)."""
+    d = load_golden("tiny_linear")
+    hp = golden_hp(d)
+    hp["verbose"] = 0
+    X, y = _frame(d)
+    np.random.seed(int(d["seed"]))
+    m = mf.KernelMF(**hp).fit(X, y)
+    T = X.iloc[:30]
+    before = m.predict(T, bound_ratings=False)
+    m.item_features[:] *= 2.0                       # same array object, new content
+    m.user_biases[0] += 0.5
+    after = m.predict(T, bound_ratings=False)
+    assert before != after
+    u = T["user_id"].map(m.user_id_map).to_numpy()
+    i = T["item_id"].map(m.item_id_map).to_numpy()
+    expect = ((m.global_mean + m.item_biases[i]) + m.user_biases[u]) + np.einsum(
+        "nk,nk->n", m.user_features[u], m.item_features[i])
+    _close(after, expect, 1e-12)
 
 
 def test_fit_empty_and_pickle(mf):
