@@ -163,6 +163,11 @@ class KernelMF(RecommenderBase):
         return state
 
     def __setstate__(self, state):
+        # build-only arguments added after a pickle was written take their
+        # defaults (the reference's pickles have none of them)
+        for key, default in (("dtype", "float64"), ("schedule", "exact"), ("device", None),
+                             ("distributed", False)):
+            state.setdefault(key, default)
         self.__dict__.update(state)
         _warn_if_no_device()
 
