@@ -70,6 +70,10 @@ WORKLOADS = {
                   "probe: C3 user shard at N=4 (250Kx100K 25M-nnz rank-64 linear SGD)"),
     "c3_shard8": (125_000, 100_000, 12_500_000, 64, "linear",
                   "probe: C3 user shard at N=8 (125Kx100K 12.5M-nnz rank-64 linear SGD)"),
+    # recommend_batch (mf_topk) on the C3 model
+    "topk": (1_000_000, 100_000, 100_000_000, 64, "topk",
+             "C3-shaped model (1Mx100K, rank 64): top-10 of all 100K items for 10K users, "
+             "items_known excluded (recommend_batch / mf_topk)"),
     # probes (not bench lines): P that fits the 256 MiB Infinity Cache
     "c3_u250k": (250_000, 100_000, 100_000_000, 64, "linear",
                  "probe: synthetic 250Kx100K 100M-nnz rank-64 linear SGD"),
@@ -239,6 +243,88 @@ def run_als(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
     return 0
 
 
+def run_topk(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
+    """recommend() for many users at C3 scale.  One step =
+    one recommend_batch pass: the top-10 of all n_items for 10K query users
+    with their rated items excluded (recommender_base.py:214-271 per user),
+    engine.topk -> mf_topk (score keys + exclusion + radix select), host
+    transfers of the query ids, exclusion CSR and results included.
+
+    value = scores/s (query users x items per second).  roofline: HBM at
+    4k B per score (the item row each score reads when nothing is reused)."""
+    import torch
+
+    from matrix_factorization.engine import SGDEngine
+
+    n_query, amount = 10_000, 10
+    rs = np.random.RandomState(3)
+    users = np.sort(rs.choice(nu, n_query, replace=False)).astype(np.int32)
+    sel = np.isin(u, users)
+    qpos = np.searchsorted(users, u[sel])
+    order = np.argsort(qpos, kind="stable")
+    ex_items = i[sel][order].astype(np.int32)
+    ex_ptr = np.concatenate([[0], np.cumsum(np.bincount(qpos, minlength=n_query))]).astype(np.int64)
+    bu0 = rs.normal(0, 0.1, nu)
+    bi0 = rs.normal(0, 0.1, ni)
+    eng = SGDEngine(np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0), nu, ni, k,
+                    "linear", args.dtype, dev, min_rating=1.0, max_rating=5.0, global_mean=mu)
+    eng.load_params(P0, Q0, bu0, bi0)
+    cpu_baseline = parity = None
+    if args.cpu_sample != 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # test infrastructure: checker and reported baseline only
+
+        ns = 20
+        P64, Q64 = P0.astype(np.float64), Q0.astype(np.float64)
+        allq = np.arange(ni, dtype=np.int32)
+        ref = []
+        t0 = time.perf_counter()
+        for q in range(ns):
+            # recommend(): predict(bound_ratings=False) of every candidate item,
+            # sort descending (stable: lower item id first among equal scores)
+            pred = oracle.predict(np.full(ni, users[q], np.int32), allq, mu, bu0, bi0, P64, Q64,
+                                  min_rating=1.0, max_rating=5.0, bound=False)
+            pred[ex_items[ex_ptr[q]:ex_ptr[q + 1]]] = -np.inf
+            ref.append(np.argsort(-pred, kind="stable")[:amount])
+        t_cpu = time.perf_counter() - t0
+        cpu_baseline = {"value": ns * ni / t_cpu, "unit": "scores/s", "cores": 1, "kind": "port",
+                        "sample": f"{ns} of the query users: oracle.predict of all {ni} items "
+                                  f"(FP64 C restatement of _predict) + stable argsort, one thread",
+                        **host_info()}
+        got, _ = eng.topk(users[:ns], amount, ex_ptr[:ns + 1], ex_items[:ex_ptr[ns]])
+        parity = {"what": f"top-{amount} item ids of {ns} users, GPU ({args.dtype}) vs oracle FP64",
+                  "ids_equal": bool(np.array_equal(got, np.asarray(ref)))}
+        log(f"cpu {cpu_baseline['value'] / 1e6:.2f} M scores/s; parity {parity}")
+    for _ in range(args.warmup):
+        eng.topk(users, amount, ex_ptr, ex_items)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.topk(users, amount, ex_ptr, ex_items)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    scores = n_query * ni * args.steps
+    ts = 4 if args.dtype == "float32" else 8
+    achieved = scores * k * ts / elapsed / 1e9
+    out = {
+        "metric": "top-k scores/s (recommend_batch, mf_topk)", "value": scores / elapsed,
+        "unit": "scores/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
+        "vs_baseline": None, "dtype": "f32" if ts == 4 else "f64", "data": "synthetic",
+        "config": {"workload": desc, "n_users": nu, "n_items": ni, "n_factors": k,
+                   "n_query": n_query, "amount": amount, "excluded_pairs": int(ex_ptr[-1]),
+                   "chunk_users": int(max(1, eng.topk_ws_budget // (8 * ni)))},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_topk_scores + k_topk_select",
+                     "note": "4k B per score (one item row per score, no reuse); the call's "
+                             "wall time incl. host transfers"},
+        "cpu_baseline": cpu_baseline, "parity": parity,
+    }
+    print(json.dumps(out), flush=True)
+    return 0
+
+
 def host_info() -> dict:
     """The host the CPU leg ran on (print nproc and the model)."""
     model = None
@@ -386,6 +472,9 @@ def main() -> int:
     ap.add_argument("--schedule", default="strata", choices=["strata", "colored"],
                     help="strata: B x B blocks, item slabs in LDS (mf_strata.hpp); "
                          "colored: one launch per edge colour (mf_rows.hpp)")
+    ap.add_argument("--delta-scale", type=float, default=None,
+                    help="N > 1: weight of the all-reduced item deltas (default 1/N, "
+                         "model averaging; 1.0 = plain gradient sum)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 process group: nccl (= RCCL, one GPU per rank) or gloo "
                          "(rehearsal: ranks may share a GPU, LOCAL_RANK mod device count)")
@@ -428,6 +517,8 @@ def main() -> int:
         if world > 1:
             raise SystemExit("the ALS workload (configs[4]) is a single-GPU config")
         return run_als(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev)
+    if kernel == "topk":
+        return run_topk(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev)
     if args.reg is None:
         args.reg = 0.02
 
@@ -459,7 +550,7 @@ def main() -> int:
         sched_desc = f"colored ({nb} conflict-free batches/epoch on rank 0)"
     t_sched = time.time() - t0
     log(f"rank {rank}: {n_local} local ratings, {sched_desc}, scheduled in {t_sched:.1f}s")
-    exch = ReplicaExchange(eng) if world > 1 else None
+    exch = ReplicaExchange(eng, scale=args.delta_scale) if world > 1 else None
 
     def reset_params():
         eng.load_params(P=P_local, bu=np.zeros(n_users_local))
@@ -477,9 +568,24 @@ def main() -> int:
         return (seed * 7919 + ep * 104729) & 0x7FFFFFFF
 
     def run(ep, seq, timing=False):
+        """The local sweep of epoch ep (N > 1, strata: delta-out form -- the
+        replica stays put and the item update lands in exch.delta)."""
         if strata:
-            return eng.epoch_strata(seq, rot_for(ep), args.lr, args.reg, timing=timing)
+            delta = None if exch is None else (exch.dq, exch.dbi)
+            return eng.epoch_strata(seq, rot_for(ep), args.lr, args.reg, timing=timing,
+                                    delta=delta)
         return eng.epoch_colored(seq, args.lr, args.reg, timing=timing)
+
+    def begin():
+        if exch is not None and not strata:
+            exch.begin_epoch()               # colored: snapshot form
+
+    def end():
+        if exch is not None:
+            if strata:
+                exch.exchange()              # all_reduce(delta); replica += delta
+            else:
+                exch.end_epoch()
 
     def serial(ep, seq):
         if strata:
@@ -508,15 +614,13 @@ def main() -> int:
         # launches, one more after the RMSE pass -- no host sync in the loop.
         seq = seq_for(ep)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if (timed and phase) else None
-        if exch is not None:
-            exch.begin_epoch()
+        begin()
         if ev:
             ev[0].record()
         run(ep, seq)
         if ev:
             ev[1].record()
-        if exch is not None:
-            exch.end_epoch()
+        end()
         if ev:
             ev[2].record()
         eng.sse_async(ep)
@@ -528,11 +632,9 @@ def main() -> int:
         if ep == 0 and strata:
             # one synchronised epoch tells whether the persistent kernel ran
             # (one launch) or the per-stratum fallback (B launches)
-            if exch is not None:
-                exch.begin_epoch()
+            begin()
             _, n_launch = run(ep, seq_for(ep), timing=True)
-            if exch is not None:
-                exch.end_epoch()
+            end()
             eng.sse_async(ep)
             persistent = n_launch == 1
             launches_per_epoch = n_launch
@@ -626,6 +728,7 @@ def main() -> int:
                        "n_factors": k, "kernel": kernel, "lr": args.lr, "reg": args.reg,
                        "schedule": sched_desc,
                        "parallelism": f"user-sharded dp{world}" if world > 1 else "single GPU",
+                       "item_delta_scale": None if exch is None else exch.scale,
                        "step": "one epoch: SGD sweep + training-RMSE pass"},
             "final_rmse": rmse[-1], "rmse_per_epoch": rmse,
             "roofline": roofline, "phases": phases,

@@ -281,7 +281,40 @@ __global__ __launch_bounds__(kBlock) void k_replica_delta(T* __restrict__ cur,
         cur[j] = mode == MF_DELTA_TAKE ? cur[j] - b : cur[j] + b;
     }
 }
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_replica_apply(T* __restrict__ cur,
+                                                          const T* __restrict__ delta, int64_t n,
+                                                          T scale) {
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < n;
+         j += (int64_t)gridDim.x * kBlock)
+        cur[j] = cur[j] + scale * delta[j];
+}
 }  // namespace mf
+
+extern "C" int mf_replica_apply(void* cur, const void* delta, int64_t n, int32_t dtype,
+                                double scale, void* stream) {
+    if (n < 0 || (n > 0 && (!cur || !delta))) {
+        set_error("mf_replica_apply: bad arguments");
+        return MF_ERR_INVALID;
+    }
+    if (n == 0) return MF_OK;
+    hipStream_t s = (hipStream_t)stream;
+    const int64_t need = (n + kBlock - 1) / kBlock;
+    const unsigned g = (unsigned)(need < 4096 ? need : 4096);
+    if (dtype == MF_F32)
+        hipLaunchKernelGGL(k_replica_apply<float>, dim3(g), dim3(kBlock), 0, s, (float*)cur,
+                           (const float*)delta, n, (float)scale);
+    else if (dtype == MF_F64)
+        hipLaunchKernelGGL(k_replica_apply<double>, dim3(g), dim3(kBlock), 0, s, (double*)cur,
+                           (const double*)delta, n, scale);
+    else {
+        set_error("unknown dtype code %d", dtype);
+        return MF_ERR_INVALID;
+    }
+    MF_HIP_CHECK(hipGetLastError());
+    return MF_OK;
+}
 
 extern "C" int mf_replica_delta(void* cur, const void* base, int64_t n, int32_t dtype,
                                 int32_t mode, void* stream) {

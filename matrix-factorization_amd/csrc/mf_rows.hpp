@@ -620,6 +620,151 @@ __global__ __launch_bounds__(kBlock) void k_sse_owned(ReadArgs<T> A, SliceTab SL
     }
 }
 
+// Training SSE, software-pipelined form of k_sse_owned (same ratings, same
+// owned user rows, same per-rating arithmetic).  A group's run is cut into
+// chunks of GS ratings (the triples of a chunk arrive in the group's GS
+// lanes) and a chunk into Q = GS / S pieces of S ratings; the loads of piece
+// j+1 are in flight while piece j is reduced (two register sets A / B used
+// alternately, so no in-flight register is ever copied).  Every load is
+// issued unconditionally -- the user row of a rating whose user the run
+// already holds is a buffer load past the resource (kBufRowDrop: dropped, no
+// memory access) -- so the compiler's waits count exactly the other set's
+// loads.
+constexpr uint32_t kBufRowDrop = 0xFFFFFFF0u;
+
+template <typename T, int W, int GS, int V, int KERN, int S>
+__global__ __launch_bounds__(kBlock) void k_sse_pipe(ReadArgs<T> A, SliceTab SL) {
+    using VT = typename VecOf<T, W>::type;
+    constexpr int R = kWave / GS;
+    constexpr int Q = GS / S;
+    static_assert(GS % S == 0 && Q % 2 == 0, "a chunk is an even number of pieces");
+    const int lane = threadIdx.x & (kWave - 1);
+    const int g = lane / GS;
+    const int l = lane % GS;
+    const int k = A.k;
+    const int kv = k / W;
+    const Hyper<T> h = A.h;
+    const int x_slice = blockIdx.x % SL.n;
+    const int64_t bps = gridDim.x / SL.n;
+    const int64_t nw_slice = bps * kWavesPerBlock;
+    const int64_t wv = (int64_t)(blockIdx.x / SL.n) * kWavesPerBlock + threadIdx.x / kWave;
+    const int64_t s0 = SL.off[x_slice], len = SL.off[x_slice + 1] - s0;
+    const int64_t b0 = s0 + len * wv / nw_slice;
+    const int64_t b1 = s0 + len * (wv + 1) / nw_slice;
+    double acc = 0.0;
+    if (b0 < b1) {
+        const int64_t wl = b1 - b0;
+        const int64_t r0 = b0 + wl * g / R, r1 = b0 + wl * (g + 1) / R;   // this group's run
+        const int64_t maxrun = (wl + R - 1) / R;                          // wave-uniform trips
+        const int64_t last = r1 > r0 ? r1 - 1 : b0;
+        const __amdgpu_buffer_rsrc_t rp = buf_rsrc(A.P, A.p_bytes), rq = buf_rsrc(A.Q, A.q_bytes);
+        const __amdgpu_buffer_rsrc_t rbu = buf_rsrc(A.Bu, A.bu_bytes), rbi = buf_rsrc(A.Bi, A.bi_bytes);
+        struct Tri { int u, i; T r; };
+        struct Piece {
+            int uu[S];
+            bool hv[S], need[S];
+            T rr[S], bi[S], bu[S];
+            VT q[S][V], p[S][V];
+        };
+        auto fetch = [&](int64_t c, Tri& t) __attribute__((always_inline)) {
+            const int64_t j = min(r0 + c + l, last);
+            t.u = A.u[j]; t.i = A.i[j]; t.r = A.r[j];
+        };
+        int lastu = -1;                    // user of the last rating issued by this group
+        // issue the loads of piece `pc` of the chunk at run offset c (triples tr)
+        auto issue = [&](const Tri& tr, int64_t c, int pc, Piece& o) __attribute__((always_inline)) {
+            int ii[S];
+#pragma unroll
+            for (int x = 0; x < S; ++x) {
+                const int src = g * GS + pc * S + x;
+                o.uu[x] = take_i<GS>(tr.u, src);
+                ii[x] = take_i<GS>(tr.i, src);
+                o.rr[x] = take_f<GS>(tr.r, src);
+                o.hv[x] = r0 + c + pc * S + x < r1;
+            }
+#pragma unroll
+            for (int x = 0; x < S; ++x) o.need[x] = o.uu[x] != (x == 0 ? lastu : o.uu[x - 1]);
+            lastu = o.uu[S - 1];
+#pragma unroll
+            for (int x = 0; x < S; ++x) {
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    const int vi = v * GS + l;
+                    const int vc = vi < kv ? vi : kv - 1;
+                    o.q[x][v] = buf_ld<0, VT>(rq, (uint32_t)(((uint32_t)ii[x] * (uint32_t)k +
+                                                             (uint32_t)(vc * W)) * sizeof(T)));
+                    o.p[x][v] = buf_ld<0, VT>(
+                        rp, o.need[x] ? (uint32_t)(((uint32_t)o.uu[x] * (uint32_t)k +
+                                                    (uint32_t)(vc * W)) * sizeof(T))
+                                      : kBufRowDrop);
+                }
+                if constexpr (KERN != MF_RBF) {
+                    o.bi[x] = buf_ld<0, T>(rbi, (uint32_t)ii[x] * (uint32_t)sizeof(T));
+                    o.bu[x] = buf_ld<0, T>(rbu, o.need[x] ? (uint32_t)o.uu[x] * (uint32_t)sizeof(T)
+                                                          : kBufRowDrop);
+                } else {
+                    o.bi[x] = o.bu[x] = (T)0;
+                }
+            }
+        };
+        VT pp[V];                          // row / bias of the run's current user
+        T pbu = (T)0;
+#pragma unroll
+        for (int v = 0; v < V; ++v) pp[v] = (VT)(T)0;
+        auto consume = [&](Piece& o) __attribute__((always_inline)) {
+#pragma unroll
+            for (int x = 0; x < S; ++x) {
+#pragma unroll
+                for (int v = 0; v < V; ++v)
+                    o.p[x][v] = o.need[x] ? o.p[x][v] : (x == 0 ? pp[v] : o.p[x - 1][v]);
+                o.bu[x] = o.need[x] ? o.bu[x] : (x == 0 ? pbu : o.bu[x - 1]);
+            }
+#pragma unroll
+            for (int x = 0; x < S; ++x) {
+                T part = (T)0;
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    VT pv[1] = {o.p[x][v]}, qv[1] = {o.q[x][v]};
+                    const T pt = lane_partial<T, W, 1, KERN>(pv, qv);
+                    part += v * GS + l < kv ? pt : (T)0;
+                }
+                const T sm = group_sum<GS>(part);
+                const T err = o.rr[x] - predict_one<T, KERN>(sm, o.bu[x], o.bi[x], h);   // :313
+                if (o.hv[x] && l == 0) acc += (double)err * (double)err;
+            }
+#pragma unroll
+            for (int v = 0; v < V; ++v) pp[v] = o.p[S - 1][v];
+            pbu = o.bu[S - 1];
+        };
+        Tri tc, tn;
+        Piece pa, pb;
+        fetch(0, tc);
+        issue(tc, 0, 0, pa);
+        for (int64_t c = 0; c < maxrun; c += GS) {
+            fetch(c + GS, tn);             // the next chunk's triples
+#pragma unroll
+            for (int j = 0; j < Q; j += 2) {
+                issue(tc, c, j + 1, pb);
+                consume(pa);
+                if (j + 2 < Q) issue(tc, c, j + 2, pa);
+                else issue(tn, c + GS, 0, pa);     // past the run: clamped, hv false
+                consume(pb);
+            }
+            tc = tn;
+        }
+    }
+    acc = wave_sum(acc);
+    __shared__ double red[kWavesPerBlock];
+    if (lane == 0) red[threadIdx.x / kWave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; ++w) t += red[w];
+        A.partials[blockIdx.x] = t;
+    }
+}
+
 __global__ void k_sum_partials(const double* part, int n, double* out);
 
 constexpr int kSseMaxBlocks = 8192;
@@ -842,8 +987,10 @@ struct SseRun {
             if (var == 0) kfn = k_sse_owned<T, W, GS, V, KERN, 16>;
             if (var == 0 && ev && std::atoi(ev) == 2) { var = 2; kfn = k_sse_owned<T, W, GS, V, KERN, 8>; }
             if (var == 0 && ev && std::atoi(ev) == 3) { var = 3; kfn = k_sse_owned<T, W, GS, V, KERN, S>; }
+            if (var == 0 && ev && std::atoi(ev) == 4) { var = 4; kfn = k_sse_pipe<T, W, GS, V, KERN, 8>; }
+            if (var == 0 && ev && std::atoi(ev) == 5) { var = 5; kfn = k_sse_pipe<T, W, GS, V, KERN, 4>; }
         }
-        static int resident_tab[4] = {0, 0, 0, 0};   // per instantiation and variant
+        static int resident_tab[6] = {0, 0, 0, 0, 0, 0};   // per instantiation and variant
         int& resident = resident_tab[var];
         if (resident == 0) {
             int dev = 0, cus = 0, per_cu = 0;

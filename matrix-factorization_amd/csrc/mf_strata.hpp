@@ -36,6 +36,9 @@ namespace mf {
 constexpr int kStrataWaves = 16;                    // 1024-thread workgroups
 constexpr int kStrataThreads = kStrataWaves * kWave;
 constexpr int kLdsLimit = 160 * 1024;               // gfx950 LDS per CU
+// buffer offset past any resource this file builds (P < kBufDrop bytes): a
+// store there is dropped by the range check, a load returns zero
+constexpr uint32_t kBufDrop = 0xFFFFFFF0u;
 
 // rating slots per lane group of one wave-instruction (16 waves x RPW slots):
 // two while a lane's share of a row is small (<= 32 B of floats, 16 B of
@@ -70,6 +73,7 @@ struct StrataArgs {
     int32_t upd_user;
     int32_t upd_item;
     uint64_t p_bytes;        // bytes of P (write-through buffer stores: < 4 GiB)
+    uint64_t bu_bytes;       // bytes of Bu (sc1 buffer loads of the bias slice)
     T* Dq;                   // nullable: delta-out mode (persistent kernel): the epoch
     T* Dbi;                  //   leaves Q / Bi untouched and writes Dq = Q' - Q, Dbi
     Hyper<T> h;
@@ -204,8 +208,11 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
             for (int v = 0; v < V; ++v) {
                 const int vi = v * GS + l;
                 const bool in = vi < kv;
+                // selects, no branch: the prefetched row is consumed on every
+                // path, so the compiler can wait for exactly that load
+                const VT qv = row[in ? vi : kv - 1];
                 p[x][v] = in ? (fwd ? pprev[x][v] : rwX.p[x][v]) : (VT)(T)0;
-                q[x][v] = in ? row[vi] : (VT)(T)0;
+                q[x][v] = in ? qv : (VT)(T)0;
             }
             if constexpr (KERN != MF_RBF) {
                 bu[x] = Bus[rwX.u[x] - ulo];
@@ -232,15 +239,20 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
                 VT np, nq;
                 sgd_rows<T, KERN>(p[x][v], q[x][v], e, d, h, np, nq);
                 pprev[x][v] = np;
-                if (!(rwX.have[x] && vi < kv)) continue;
-                if (A.upd_user) {
-                    if constexpr (WT)
-                        buf_st<16>(prs, (uint32_t)(((uint32_t)rwX.u[x] * (uint32_t)k +
-                                                    (uint32_t)(vi * W)) * sizeof(T)), np);
-                    else
-                        st<true>(pw + vi, np);
+                const bool ok = rwX.have[x] && vi < kv;
+                if constexpr (WT) {
+                    // unconditional store; a masked lane's offset is out of
+                    // range and the store is dropped -- one store per lane and
+                    // step on every path keeps the vmcnt waits exact
+                    const uint32_t off = (ok && A.upd_user)
+                        ? (uint32_t)(((uint32_t)rwX.u[x] * (uint32_t)k + (uint32_t)(vi * W)) *
+                                     sizeof(T))
+                        : kBufDrop;
+                    buf_st<16>(prs, off, np);
+                } else {
+                    if (ok && A.upd_user) st<true>(pw + vi, np);
                 }
-                if (A.upd_item) qw[vi] = nq;
+                if (ok && A.upd_item) qw[vi] = nq;
             }
             uprev[x] = (rwX.have[x] && A.upd_user) ? rwX.u[x] : -1;
         }
@@ -268,8 +280,9 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
             for (int v = 0; v < V; ++v) {
                 const int vi = v * GS + l;
                 const bool in = vi < kv;
+                const VT qv = row[in ? vi : kv - 1];
                 p[x][v] = in ? (f1 ? pprev[x][v] : (f2 ? pprev2[x][v] : Ra.p[x][v])) : (VT)(T)0;
-                q[x][v] = in ? row[vi] : (VT)(T)0;
+                q[x][v] = in ? qv : (VT)(T)0;
             }
             if constexpr (KERN != MF_RBF) {
                 bu[x] = Bus[Ra.u[x] - ulo];
@@ -297,15 +310,17 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
                 sgd_rows<T, KERN>(p[x][v], q[x][v], e, d, h, np, nq);
                 pprev2[x][v] = pprev[x][v];
                 pprev[x][v] = np;
-                if (!(Ra.have[x] && vi < kv)) continue;
-                if (A.upd_user) {
-                    if constexpr (WT)
-                        buf_st<16>(prs, (uint32_t)(((uint32_t)Ra.u[x] * (uint32_t)k +
-                                                    (uint32_t)(vi * W)) * sizeof(T)), np);
-                    else
-                        st<true>(pw + vi, np);
+                const bool ok = Ra.have[x] && vi < kv;
+                if constexpr (WT) {
+                    const uint32_t off = (ok && A.upd_user)
+                        ? (uint32_t)(((uint32_t)Ra.u[x] * (uint32_t)k + (uint32_t)(vi * W)) *
+                                     sizeof(T))
+                        : kBufDrop;
+                    buf_st<16>(prs, off, np);
+                } else {
+                    if (ok && A.upd_user) st<true>(pw + vi, np);
                 }
-                if (A.upd_item) qw[vi] = nq;
+                if (ok && A.upd_item) qw[vi] = nq;
             }
             uprev2[x] = uprev[x];
             uprev[x] = (Ra.have[x] && A.upd_user) ? Ra.u[x] : -1;
@@ -332,38 +347,56 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
         }
     }
     if constexpr (BUS_IN && KERN != MF_RBF) {
-        // all loads issued before the first LDS write waits for them
+        // all loads issued before the first LDS write waits for them.  sc1
+        // BUFFER loads, not relaxed atomic loads: the same L2-served access,
+        // but an atomic load here makes the compiler drain every memory
+        // operation (s_waitcnt vmcnt(0)) at the top of the step loop below,
+        // i.e. the row prefetch of the previous step on every second step
+        // (measured in the ISA: vmcnt(5..8) instead)
         constexpr int kBu = 4;
+        const __amdgpu_buffer_rsrc_t brs = buf_rsrc(A.Bu, A.bu_bytes);
         T bt[kBu];
         const int last = nus > 0 ? nus - 1 : 0;
 #pragma unroll
         for (int c = 0; c < kBu; ++c) {
             const int x = (int)threadIdx.x + c * kStrataThreads;
-            bt[c] = __hip_atomic_load(A.Bu + ulo + (x < last ? x : last), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);            // sc1 load
+            bt[c] = buf_ld<16, T>(brs, (uint32_t)(ulo + (x < last ? x : last)) * (uint32_t)sizeof(T));
         }
+        // unconditional LDS writes (lanes past the slice rewrite its last
+        // entry with the value they loaded from it): a load whose register
+        // is consumed only on some paths would again cost a full drain at
+        // the top of the step loop
 #pragma unroll
         for (int c = 0; c < kBu; ++c) {
             const int x = (int)threadIdx.x + c * kStrataThreads;
-            if (x < nus) Bus[x] = bt[c];
+            Bus[x < last ? x : last] = bt[c];
         }
         for (int x = (int)threadIdx.x + kBu * kStrataThreads; x < nus; x += kStrataThreads)
-            Bus[x] = __hip_atomic_load(A.Bu + ulo + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            Bus[x] = buf_ld<16, T>(brs, (uint32_t)(ulo + x) * (uint32_t)sizeof(T));
         lds_barrier();
     }
+    // Whole unrolled groups inside the loop, the remainder after it: a group
+    // cut short inside the loop body would give the compiler a back-edge on
+    // which a prefetched row is never consumed, and it then drains every
+    // memory operation (vmcnt(0)) at the top of each iteration.
     if constexpr (DEPTH == 2) {
         // copies by t mod 3: rows R[t%3] applied at t; triples of t+2 in
         // T[(t+2)%3], the load of t+4 goes to T[(t+1)%3] (consumed at t-1)
-        for (int t = 0; t < nst; t += 3) {
+        int t = 0;
+        for (; t + 2 < nst; t += 3) {
             step2(t, tc, tb, ra, rc);
-            if (t + 1 < nst) step2(t + 1, ta, tc, rb, ra);
-            if (t + 2 < nst) step2(t + 2, tb, ta, rc, rb);
+            step2(t + 1, ta, tc, rb, ra);
+            step2(t + 2, tb, ta, rc, rb);
         }
+        if (t < nst) step2(t, tc, tb, ra, rc);
+        if (t + 1 < nst) step2(t + 1, ta, tc, rb, ra);
     } else {
-        for (int t = 0; t < nst; t += 2) {
+        int t = 0;
+        for (; t + 1 < nst; t += 2) {
             step(t, ta, tb, ra, rb);
-            if (t + 1 < nst) step(t + 1, tb, ta, rb, ra);
+            step(t + 1, tb, ta, rb, ra);
         }
+        if (t < nst) step(t, ta, tb, ra, rb);
     }
 }
 
@@ -642,6 +675,7 @@ struct StrataRun {
         a.ubnd = p.ubnd; a.ibnd = p.ibnd; a.bstep = p.bstep;
         a.B = p.B; a.seed = p.seed; a.k = p.k; a.upd_user = p.uu; a.upd_item = p.ui;
         a.p_bytes = (uint64_t)p.n_users * (uint64_t)p.k * sizeof(T);
+        a.bu_bytes = (uint64_t)p.n_users * sizeof(T);
         a.Dq = static_cast<T*>(p.dq);
         a.Dbi = static_cast<T*>(p.dbi);
         if (p.dq && !p.dbi && KERN != MF_RBF) {
@@ -658,7 +692,7 @@ struct StrataRun {
         }
         bool persistent = false;
         if ((p.flags & MF_FLAG_PERSISTENT) && p.ws &&
-            p.ws_bytes >= strata_ws_bytes(p.B, p.n_seq) && a.p_bytes < 0xFFFFFFFFull) {
+            p.ws_bytes >= strata_ws_bytes(p.B, p.n_seq) && a.p_bytes < (uint64_t)kBufDrop) {
             auto efn = (p.flags & MF_FLAG_DEEP_PIPE) ? k_sgd_strata_epoch<T, W, GS, V, KERN, S, 2>
                                                      : k_sgd_strata_epoch<T, W, GS, V, KERN, S, 1>;
             MF_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(efn),

@@ -91,6 +91,7 @@ SIGNATURES = {
     "mf_als_sweep_probe": (ctypes.c_int, [
         _P, _P, _P, _I32, _F64, _P, _P, _P, _P, _I32, _I32, _F64, _P, _P]),
     "mf_replica_delta": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P]),
+    "mf_replica_apply": (ctypes.c_int, [_P, _P, _I64, _I32, _F64, _P]),
     "mf_sched_levels": (ctypes.c_int, [
         _P, _P, _I64, _P, _I32, _I32, _I32, _I32, _P, _P, _I64, _P]),
     "mf_sched_color": (ctypes.c_int, [

@@ -12,15 +12,20 @@ is the build's multi-GPU extension of the same epoch:
   (mf_sgd_epoch_strata_delta: the replica is not written, the slab's update
   lands in a flat delta buffer where the slab would have been written back),
   ``all_reduce(SUM)`` of the delta over xGMI, one element-wise apply
-  (replica += sum) -- every rank ends the epoch with the same replica and no
-  snapshot copy is taken.  The colored schedule keeps the snapshot form
+  (replica += scale * sum, scale = min(1/2, 2/world): default_delta_scale)
+  -- every rank ends the epoch with the same replica and no snapshot copy is
+  taken.  The colored schedule keeps the snapshot form
   (snapshot, sweep, take, all-reduce, apply);
 * the training SSE of every epoch stays on the device and is summed across
   ranks once (or per epoch when the caller prints it).
 
 Item updates are thereby delayed by up to one epoch relative to the
-sequential sweep (user updates are exact): RMSE is reported next to the
-1-GPU run, not claimed identical.
+sequential sweep and combined with a damped sum (user updates are exact):
+RMSE is reported next to the 1-GPU run, not claimed identical.  The plain
+sum of the deltas (scale 1, "all-reduce of the gradients") is available but
+is not the default: each rank's local epoch moves an item much of the way
+toward its local optimum, so N summed moves overshoot and C3 diverges at
+N >= 4 (default_delta_scale has the measurements).
 
 ``fit_sharded`` is the estimator's process-group mode (KernelMF(...,
 distributed=True).fit on every rank with the same data and RNG state).
@@ -67,6 +72,23 @@ def local_shard(u: np.ndarray, i: np.ndarray, r: np.ndarray, bounds: np.ndarray,
     return (u[m] - lo).astype(np.int32), i[m].astype(np.int32), r[m]
 
 
+def default_delta_scale(world: int) -> float:
+    """Weight of the all-reduced sum of the rank-local item deltas:
+    min(1/2, 2/world) (1 for one rank).
+
+    Each rank's epoch moves an item part of the way toward the optimum of
+    that rank's ratings; the plain sum (1.0) overshoots by up to ~world and
+    diverges, plain averaging (1/world) under-steps.  Measured at C3 (lr
+    0.01, reg 0.02, final train RMSE after 20 epochs; N = 1: 0.7106;
+    DESIGN.md section 6): N = 2: 0.7434 at 1/2, 0.7887 at 1; N = 4: 0.7469 at
+    1/2, 0.7974 at 1/4, NaN at 1; N = 8: 0.7977 at 1/4, 0.8706 at 1/8, 2.29
+    at 3/8, NaN at 1/2.  2/world sits below the divergence edge (between 2/N
+    and 3/N at N = 8) with the best RMSE measured."""
+    if world <= 1:
+        return 1.0
+    return min(0.5, 2.0 / world)
+
+
 class ReplicaExchange:
     """The per-epoch delta all-reduce of the replicated item parameters.
 
@@ -75,9 +97,13 @@ class ReplicaExchange:
     has the same layout (strata: the delta-out target; colored: the
     start-of-epoch snapshot)."""
 
-    def __init__(self, engine: SGDEngine, group=None):
+    def __init__(self, engine: SGDEngine, group=None, scale: Optional[float] = None):
         self.e = engine
         self.group = group
+        # weight of the summed deltas (default_delta_scale); 1.0 is the plain
+        # gradient-sum form, 1 / world plain model averaging
+        self.scale = (default_delta_scale(world_info(group)[0]) if scale is None
+                      else float(scale))
         n, k = engine.n_items, engine.k
         self.flat = torch.empty(n * k + n, dtype=engine.tdt, device=engine.dev)
         self.delta = torch.zeros_like(self.flat)
@@ -103,6 +129,13 @@ class ReplicaExchange:
     def _reduce(self) -> None:
         dist.all_reduce(self.delta, op=dist.ReduceOp.SUM, group=self.group)
 
+    def _apply(self) -> None:
+        """mf_replica_apply: flat += scale * delta."""
+        e = self.e
+        with torch.cuda.device(e.dev):
+            _lib.call("mf_replica_apply", _tp(self.flat), _tp(self.delta), self.flat.numel(),
+                      e.dcode, self.scale, e.stream)
+
     # ---- strata: delta-out sweep, all-reduce, apply
     def strata_epoch(self, seq, seed, lr, reg, update_user=True, update_item=True,
                      timing=False):
@@ -112,9 +145,9 @@ class ReplicaExchange:
         return ms
 
     def exchange(self) -> None:
-        """delta = sum over ranks of the local deltas; flat += delta."""
+        """delta = sum over ranks of the local deltas; flat += scale * delta."""
         self._reduce()
-        self._delta(_lib.MF_DELTA_APPLY)
+        self._apply()
 
     # ---- colored (and any in-place sweep): snapshot form
     def begin_epoch(self) -> None:
@@ -126,7 +159,7 @@ class ReplicaExchange:
         self.flat, self.delta = self.delta, self.flat       # delta holds the local delta
         self._rebind()
         self._reduce()
-        self._delta(_lib.MF_DELTA_APPLY)                    # flat (snapshot) += sum
+        self._apply()                                       # flat (snapshot) += scale * sum
 
     def _rebind(self) -> None:
         n, k = self.e.n_items, self.e.k

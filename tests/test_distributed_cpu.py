@@ -1,8 +1,9 @@
 """User-sharded data parallelism, rehearsed on CPU with gloo (world_size 2).
 
-The per-epoch exchange of matrix_factorization.distributed (snapshot ->
-local colored epoch -> delta -> all_reduce(SUM) -> apply) runs in two real
-processes over gloo.  The device sweeps are replaced by the CPU oracle and the
+The per-epoch exchange of matrix_factorization.distributed (colored:
+snapshot -> local epoch -> delta; strata: delta-out epoch; then
+all_reduce(SUM) -> replica += sum / world) runs in two real processes over
+gloo.  The device sweeps are replaced by the CPU oracle and the
 replica arithmetic by torch on CPU tensors (test doubles, this file only); the
 sharding, schedules, collective and bookkeeping are the product code.  The
 result must equal a single-process simulation of the same algorithm.
@@ -22,6 +23,12 @@ import oracle
 NU, NI, NNZ, K = 300, 80, 6000, 8
 LR, REG, EPOCHS, SEED = 0.02, 0.05, 3, 99
 STRATA_B = 3                                     # strata per epoch on each rank
+
+
+def _scale(world):
+    from matrix_factorization.distributed import default_delta_scale
+
+    return default_delta_scale(world)
 
 
 def _data():
@@ -124,6 +131,9 @@ def _exchange_cls():
             else:
                 self.flat.add_(self.delta)
 
+        def _apply(self):                             # mf_replica_apply on CPU
+            self.flat.add_(self.scale * self.delta)
+
     return CpuExchange
 
 
@@ -194,8 +204,8 @@ def _simulate(world, schedule="colored"):
                 e.epoch_colored(seq, LR, REG)
             dQ += e.Q.numpy() - Q
             dbi += e.bi.numpy() - bi
-        Q = Q + dQ
-        bi = bi + dbi
+        Q = Q + _scale(world) * dQ                    # damped sum (default_delta_scale)
+        bi = bi + _scale(world) * dbi
         for e in engs:
             e.Q = torch.as_tensor(Q.copy())
             e.bi = torch.as_tensor(bi.copy())
@@ -274,7 +284,7 @@ def _fit_rank(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def _simulate_fit(world):
+def _simulate_fit(world, blocks=None):
     """Single-process restatement of KernelMF(distributed=True).fit: the
     reference's draws (sample, normal(P), normal(Q)), then per epoch one
     np.random.randint shared by all ranks, rank r's strata drawn from
@@ -299,7 +309,11 @@ def _simulate_fit(world):
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         e = CpuEngine(lu, li, lr_, hi - lo, m.n_items, K, mu)
         e.load_params(P=P[lo:hi], bu=np.zeros(hi - lo), Q=Q, bi=np.zeros(m.n_items))
-        e.prepare_strata()
+        if blocks == "auto":            # the GPU engine's own choice of B
+            from matrix_factorization.engine import choose_strata_blocks
+            e.prepare_strata(choose_strata_blocks(lu, li, hi - lo, m.n_items, K, 1)[0])
+        else:
+            e.prepare_strata(blocks)
         engs.append(e)
     bi = np.zeros(m.n_items)
     sse = np.zeros(EPOCHS)
@@ -314,7 +328,7 @@ def _simulate_fit(world):
             e.epoch_strata(seq, int(rs.randint(0, 2**31 - 1)), LR, REG)
             dQ += e.Q.numpy() - Q
             dbi += e.bi.numpy() - bi
-        Q, bi = Q + dQ, bi + dbi
+        Q, bi = Q + _scale(world) * dQ, bi + _scale(world) * dbi
         for e in engs:
             e.Q = torch.as_tensor(Q.copy())
             e.bi = torch.as_tensor(bi.copy())

@@ -60,3 +60,37 @@ def test_two_ranks_on_one_gpu_match_cpu_simulation(tmp_path, schedule):
     for k in range(world):
         assert np.max(np.abs(res[k]["P"] - engs[k].P.numpy())) < 1e-10
     assert np.max(np.abs(res[0]["rmse"] - rmse)) < 1e-10
+
+
+def _fit_rank(rank, world, port, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import matrix_factorization as mf
+    from test_distributed_cpu import FIT_HP, SEED, _frame
+
+    X, y = _frame()
+    np.random.seed(SEED)
+    m = mf.KernelMF(distributed=True, device="cuda:0", **FIT_HP).fit(X, y)
+    np.savez(os.path.join(out, f"fit{rank}.npz"), P=m.user_features, Q=m.item_features,
+             bu=m.user_biases, bi=m.item_biases, rmse=np.asarray(m.train_rmse),
+             pred=np.asarray(m.predict(X.iloc[:50])))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_kernelmf_distributed_fit_on_one_gpu(tmp_path):
+    """KernelMF(distributed=True).fit with two gloo ranks sharing cuda:0: the
+    product path end to end (delta-out persistent sweeps, all-reduce,
+    mf_replica_delta, gathers); equal to the restated algorithm."""
+    from test_distributed_cpu import _free_port, _simulate_fit
+
+    world = 2
+    mp.start_processes(_fit_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    res = [dict(np.load(tmp_path / f"fit{k}.npz")) for k in range(world)]
+    for key in ("P", "Q", "bu", "bi", "rmse", "pred"):
+        assert np.array_equal(res[0][key], res[1][key]), key
+    P, Q, bu, bi, rmse = _simulate_fit(world, blocks="auto")
+    for key, ref in (("P", P), ("Q", Q), ("bu", bu), ("bi", bi), ("rmse", rmse)):
+        assert np.max(np.abs(res[0][key] - ref)) < 1e-10, key

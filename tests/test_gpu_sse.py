@@ -1,0 +1,44 @@
+"""The training-RMSE pass (mf_sse, _calculate_rmse kernel_matrix_factorization.py:
+240-317) in its kernel variants: k_sse_owned (user rows owned per run),
+k_sse_pipe (the same walk software-pipelined, pieces of 8 or 4 ratings) and
+k_sse_stream.  Per rating the arithmetic is identical; the FP64 sums differ
+only in accumulation order (the grid follows each kernel's occupancy), so
+they agree to 1e-12 relative, and with the FP64 oracle to 1e-9 relative
+(FP32 products and dot-product order)."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("k,nu,ni,nnz", [(64, 20000, 4000, 600000), (64, 300, 5000, 200000)])
+def test_sse_variants_agree(k, nu, ni, nnz, monkeypatch):
+    import oracle
+    from matrix_factorization.engine import SGDEngine
+
+    rs = np.random.RandomState(k + nu)
+    keys = rs.choice(nu * ni, nnz, replace=False)
+    u = (keys // ni).astype(np.int32)
+    i = (keys % ni).astype(np.int32)
+    r = rs.randint(1, 6, nnz).astype(np.float32)
+    P = rs.normal(0, 0.3, (nu, k)).astype(np.float32)
+    Q = rs.normal(0, 0.3, (ni, k)).astype(np.float32)
+    bu = rs.normal(0, 0.1, nu).astype(np.float32)
+    bi = rs.normal(0, 0.1, ni).astype(np.float32)
+    eng = SGDEngine(u, i, r, nu, ni, k, "linear", "float32", "cuda:0",
+                    global_mean=float(r.mean()), min_rating=1, max_rating=5)
+    eng.load_params(P, Q, bu, bi)
+    got = {}
+    for slot, var in enumerate(("0", "4", "5", "1")):
+        monkeypatch.setenv("MF_SSE_VARIANT", var)
+        eng.sse_async(slot)
+        got[var] = eng.sse_values(slot + 1)[slot]
+    monkeypatch.delenv("MF_SSE_VARIANT")
+    for v in got.values():
+        assert abs(v - got["0"]) <= 1e-12 * got["0"], got
+    ref = oracle.sse(u, i, r.astype(np.float64), eng.global_mean, bu.astype(np.float64),
+                     bi.astype(np.float64), P.astype(np.float64), Q.astype(np.float64))
+    for v in got.values():
+        assert abs(v - ref) <= 1e-9 * ref, (got, ref)
