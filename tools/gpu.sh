@@ -19,6 +19,7 @@
 #   dist:N[:ARGS]        torch.distributed.run N gloo ranks on this one GPU:
 #                        python bench.py --gpus N --backend gloo ARGS
 #   env:VAR=VAL          export VAR=VAL for the following steps (VAL empty: unset)
+#   counters             rocprofv3 -L (the counters this GPU offers) -> NN_counters.txt
 set -e
 TAG=$1; shift
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -69,6 +70,8 @@ for step in "$@"; do
         timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$nr" \
             --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus "$nr" --backend gloo \
             ${dargs//,/ } > "$p.json" 2> "$p.log" ;;
+    counters)
+        timeout -k 10 120 rocprofv3 -L > "$p.txt" 2>&1 ;;
     env)
         var=${rest%%=*}; val=${rest#*=}
         if [ -z "$val" ]; then unset "$var"; else export "$var=$val"; fi ;;
