@@ -295,12 +295,15 @@ def run_topk(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
         parity = {"what": f"top-{amount} item ids of {ns} users, GPU ({args.dtype}) vs oracle FP64",
                   "ids_equal": bool(np.array_equal(got, np.asarray(ref)))}
         log(f"cpu {cpu_baseline['value'] / 1e6:.2f} M scores/s; parity {parity}")
+    # inputs resident in HBM (query ids, sorted exclusion CSR), results left
+    # on the device: the timed region is the mf_topk launches
+    batch = eng.topk_prepare(users, amount, ex_ptr, ex_items)
     for _ in range(args.warmup):
-        eng.topk(users, amount, ex_ptr, ex_items)
+        eng.topk_launch(batch)
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.topk(users, amount, ex_ptr, ex_items)
+        eng.topk_launch(batch)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     scores = n_query * ni * args.steps
@@ -313,12 +316,14 @@ def run_topk(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
         "vs_baseline": None, "dtype": "f32" if ts == 4 else "f64", "data": "synthetic",
         "config": {"workload": desc, "n_users": nu, "n_items": ni, "n_factors": k,
                    "n_query": n_query, "amount": amount, "excluded_pairs": int(ex_ptr[-1]),
-                   "chunk_users": int(max(1, eng.topk_ws_budget // (8 * ni)))},
+                   "chunk_users": batch["chunk"],
+                   "path": "two-stage (keys in HBM)" if os.environ.get("MF_TOPK_TWO_STAGE") == "1"
+                           else "fused (k_topk_fused + k_topk_merge)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                      "kernel": "k_topk_scores + k_topk_select",
-                     "note": "4k B per score (one item row per score, no reuse); the call's "
-                             "wall time incl. host transfers"},
+                     "note": "4k B per score (one item row per score, no reuse); device "
+                             "time of the mf_topk launches (inputs resident)"},
         "cpu_baseline": cpu_baseline, "parity": parity,
     }
     print(json.dumps(out), flush=True)
@@ -469,6 +474,8 @@ def main() -> int:
                     help="do not bracket the SGD / RMSE phases with hipEvents")
     ap.add_argument("--blocks", type=int, default=None,
                     help="strata: B (probes; default: engine.choose_strata_blocks)")
+    ap.add_argument("--waves", type=int, default=None, choices=[8, 16],
+                    help="strata: waves per workgroup (default: by the plan's slot fill)")
     ap.add_argument("--schedule", default="strata", choices=["strata", "colored"],
                     help="strata: B x B blocks, item slabs in LDS (mf_strata.hpp); "
                          "colored: one launch per edge colour (mf_rows.hpp)")
@@ -486,7 +493,7 @@ def main() -> int:
     from matrix_factorization import _lib
     from matrix_factorization.distributed import (ReplicaExchange, global_rmse,
                                                   local_shard, shard_users)
-    from matrix_factorization.engine import SGDEngine
+    from matrix_factorization.engine import SGDEngine, strata_slots
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -537,12 +544,13 @@ def main() -> int:
     t0 = time.time()
     strata = args.schedule == "strata"
     if strata:
-        plan = eng.prepare_strata(n_blocks=args.blocks)
+        plan = eng.prepare_strata(n_blocks=args.blocks, waves=args.waves)
         nb = plan.B
         strat_sizes = plan.stratum_sizes()           # ratings per stratum (launch)
         fill = n_local / max(plan.n_positions, 1)
         sched_desc = (f"strata (B={nb}: {nb} launches/epoch, item slabs in LDS, "
-                      f"{plan.NS} user-owned slots x {int(plan.n_steps.max())} steps max "
+                      f"{plan.NS} user-owned slots ({plan.NS * 1024 // strata_slots(k, eng.dcode)} "
+                      f"threads/workgroup) x {int(plan.n_steps.max())} steps max "
                       f"per block, {fill:.1%} slot fill)")
     else:
         nb = eng.prepare_colored()

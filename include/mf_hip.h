@@ -208,6 +208,11 @@ int mf_strata_set_probe(int64_t* probe);
 /* Rating slots per step of the strata kernel for (n_factors, dtype); -1 on
  * invalid arguments. */
 int32_t mf_strata_slots(int32_t n_factors, int32_t dtype);
+/* The same for a workgroup of `waves` waves: 16 (the default) or, FP32 with
+ * n_factors <= 64 only, 8 -- a plan built with that many slots runs the
+ * 8-wave kernels (blocks whose step count is set by the item degree, not by
+ * the slot count); -1 where the layout has no 8-wave kernels. */
+int32_t mf_strata_slots_waves(int32_t n_factors, int32_t dtype, int32_t waves);
 
 /*
  * Sum of squared training errors, sum_j (r_j - pred_j)^2, accumulated in

@@ -283,17 +283,23 @@ extern "C" int mf_strata_status(const void* workspace, int32_t n_blocks, void* s
     return MF_OK;
 }
 
-extern "C" int32_t mf_strata_slots(int32_t n_factors, int32_t dtype) {
-    if (n_factors < 0 || n_factors > kMaxFactors || (dtype != MF_F32 && dtype != MF_F64)) {
-        set_error("mf_strata_slots: n_factors=%d / dtype=%d invalid", n_factors, dtype);
+extern "C" int32_t mf_strata_slots_waves(int32_t n_factors, int32_t dtype, int32_t waves) {
+    if (n_factors < 0 || n_factors > kMaxFactors || (dtype != MF_F32 && dtype != MF_F64) ||
+        (waves != 16 && waves != 8)) {
+        set_error("mf_strata_slots_waves: n_factors=%d / dtype=%d / waves=%d invalid", n_factors,
+                  dtype, waves);
         return -1;
     }
     if (dtype == MF_F32) {
-        StrataSlots<float> f;
+        StrataSlots<float> f{waves};
         return dispatch_rows<float>(n_factors, MF_LINEAR, f);
     }
-    StrataSlots<double> f;
+    StrataSlots<double> f{waves};
     return dispatch_rows<double>(n_factors, MF_LINEAR, f);
+}
+
+extern "C" int32_t mf_strata_slots(int32_t n_factors, int32_t dtype) {
+    return mf_strata_slots_waves(n_factors, dtype, 16);
 }
 
 static int strata_epoch(const int32_t* user_ids, const int32_t* item_ids,

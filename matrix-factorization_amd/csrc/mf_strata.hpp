@@ -29,6 +29,8 @@
 // bias slices amortise over the block's ratings.
 #pragma once
 
+#include <type_traits>
+
 #include "mf_rows.hpp"
 
 namespace mf {
@@ -49,9 +51,9 @@ constexpr int strata_group_slots() {
     constexpr int bytes = W * V * (int)sizeof(T);
     return ((kWave / GS) < 8 && bytes <= (sizeof(T) == 4 ? 32 : 16)) ? 2 : 1;
 }
-template <typename T, int W, int GS, int V>
+template <typename T, int W, int GS, int V, int NW = kStrataWaves>
 constexpr int strata_slots() {
-    return kStrataWaves * strata_group_slots<T, W, GS, V>() * (kWave / GS);
+    return NW * strata_group_slots<T, W, GS, V>() * (kWave / GS);
 }
 
 template <typename T>
@@ -118,14 +120,15 @@ __device__ __forceinline__ void lds_barrier() {
 // and t+4 -- for blocks of few steps, where each step otherwise waits one
 // load latency).
 template <typename T, int W, int GS, int V, int KERN, int S, bool WT = false, bool BUS_IN = false,
-          int DEPTH = 1>
+          int DEPTH = 1, int NW = kStrataWaves>
 __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk, int ulo, int ilo,
                                              T* Qs, T* Bis, T* Bus, const Hyper<T> h,
                                              int nus = 0) {
     using VT = typename VecOf<T, W>::type;
     constexpr int R = kWave / GS;
     constexpr int RPW = S * R;
-    constexpr int NS = kStrataWaves * RPW;
+    constexpr int NS = NW * RPW;
+    constexpr int TH = NW * kWave;                  // threads of the workgroup
     const int k = A.k;
     const int kv = k / W;
     [[maybe_unused]] __amdgpu_buffer_rsrc_t prs;
@@ -359,7 +362,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
         const int last = nus > 0 ? nus - 1 : 0;
 #pragma unroll
         for (int c = 0; c < kBu; ++c) {
-            const int x = (int)threadIdx.x + c * kStrataThreads;
+            const int x = (int)threadIdx.x + c * TH;
             bt[c] = buf_ld<16, T>(brs, (uint32_t)(ulo + (x < last ? x : last)) * (uint32_t)sizeof(T));
         }
         // unconditional LDS writes (lanes past the slice rewrite its last
@@ -368,10 +371,10 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
         // the top of the step loop
 #pragma unroll
         for (int c = 0; c < kBu; ++c) {
-            const int x = (int)threadIdx.x + c * kStrataThreads;
+            const int x = (int)threadIdx.x + c * TH;
             Bus[x < last ? x : last] = bt[c];
         }
-        for (int x = (int)threadIdx.x + kBu * kStrataThreads; x < nus; x += kStrataThreads)
+        for (int x = (int)threadIdx.x + kBu * TH; x < nus; x += TH)
             Bus[x] = buf_ld<16, T>(brs, (uint32_t)(ulo + x) * (uint32_t)sizeof(T));
         lds_barrier();
     }
@@ -401,7 +404,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
 }
 
 // Stage the item slab (+ biases) of item range [ilo, ilo + nqi).
-template <typename T, int W, int KERN>
+template <typename T, int W, int KERN, int TH = kStrataThreads>
 __device__ __forceinline__ void strata_stage_slab(const StrataArgs<T>& A, int ilo, int nqi, T* Qs,
                                                   T* Bis) {
     using VT = typename VecOf<T, W>::type;
@@ -410,13 +413,13 @@ __device__ __forceinline__ void strata_stage_slab(const StrataArgs<T>& A, int il
     VT* dst = reinterpret_cast<VT*>(Qs);
     const int nv = nqi * (k / W);
 #pragma unroll 4
-    for (int t = threadIdx.x; t < nv; t += kStrataThreads) dst[t] = src[t];
+    for (int t = threadIdx.x; t < nv; t += TH) dst[t] = src[t];
     if constexpr (KERN != MF_RBF)
-        for (int t = threadIdx.x; t < nqi; t += kStrataThreads) Bis[t] = A.Bi[ilo + t];
+        for (int t = threadIdx.x; t < nqi; t += TH) Bis[t] = A.Bi[ilo + t];
 }
 
 // Write the item slab (+ biases) back.
-template <typename T, int W, int KERN>
+template <typename T, int W, int KERN, int TH = kStrataThreads>
 __device__ __forceinline__ void strata_store_slab(const StrataArgs<T>& A, int ilo, int nqi,
                                                   const T* Qs, const T* Bis) {
     using VT = typename VecOf<T, W>::type;
@@ -426,16 +429,16 @@ __device__ __forceinline__ void strata_store_slab(const StrataArgs<T>& A, int il
     const VT* src = reinterpret_cast<const VT*>(Qs);
     const int nv = nqi * (k / W);
 #pragma unroll 4
-    for (int t = threadIdx.x; t < nv; t += kStrataThreads) dst[t] = src[t];
+    for (int t = threadIdx.x; t < nv; t += TH) dst[t] = src[t];
     if constexpr (KERN != MF_RBF)
-        for (int t = threadIdx.x; t < nqi; t += kStrataThreads) A.Bi[ilo + t] = Bis[t];
+        for (int t = threadIdx.x; t < nqi; t += TH) A.Bi[ilo + t] = Bis[t];
 }
 
 // Delta-out end of the persistent epoch (user-sharded multi-GPU): Q and Bi
 // were not written during the epoch (the slab lived in LDS), so the local
 // update of this slab is LDS - global; it goes to Dq / Dbi and the replica
 // stays at its start-of-epoch value for the exchange to update.
-template <typename T, int W, int KERN>
+template <typename T, int W, int KERN, int TH = kStrataThreads>
 __device__ __forceinline__ void strata_delta_slab(const StrataArgs<T>& A, int ilo, int nqi,
                                                   const T* Qs, const T* Bis) {
     using VT = typename VecOf<T, W>::type;
@@ -445,9 +448,9 @@ __device__ __forceinline__ void strata_delta_slab(const StrataArgs<T>& A, int il
     const VT* src = reinterpret_cast<const VT*>(Qs);
     const int nv = nqi * (k / W);
 #pragma unroll 4
-    for (int t = threadIdx.x; t < nv; t += kStrataThreads) dst[t] = src[t] - q0[t];
+    for (int t = threadIdx.x; t < nv; t += TH) dst[t] = src[t] - q0[t];
     if constexpr (KERN != MF_RBF)
-        for (int t = threadIdx.x; t < nqi; t += kStrataThreads)
+        for (int t = threadIdx.x; t < nqi; t += TH)
             A.Dbi[ilo + t] = Bis[t] - A.Bi[ilo + t];
 }
 
@@ -481,8 +484,9 @@ __device__ __forceinline__ Hyper<double> hyper_regs(const Hyper<double>& s) {
 }
 
 // One stratum per launch: workgroup w applies block (A.s, w).
-template <typename T, int W, int GS, int V, int KERN, int S>
-__global__ __launch_bounds__(kStrataThreads) void k_sgd_strata(StrataArgs<T> A) {
+template <typename T, int W, int GS, int V, int KERN, int S, int NW = kStrataWaves>
+__global__ __launch_bounds__(NW * kWave) void k_sgd_strata(StrataArgs<T> A) {
+    constexpr int TH = NW * kWave;
     extern __shared__ __align__(16) unsigned char smem[];
     const int B = A.B;
     const int w = blockIdx.x;
@@ -493,16 +497,16 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata(StrataArgs<T> A) 
     T* Qs = reinterpret_cast<T*>(smem);
     T* Bis = Qs + (size_t)nqi * A.k;
     T* Bus = Bis + nqi;
-    strata_stage_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
+    strata_stage_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
     if constexpr (KERN != MF_RBF)
-        for (int t = threadIdx.x; t < nus; t += kStrataThreads) Bus[t] = A.Bu[ulo + t];
+        for (int t = threadIdx.x; t < nus; t += TH) Bus[t] = A.Bu[ulo + t];
     __syncthreads();
-    strata_block<T, W, GS, V, KERN, S>(A, blk, ulo, ilo, Qs, Bis, Bus, hyper_regs(A.h));
+    strata_block<T, W, GS, V, KERN, S, false, false, 1, NW>(A, blk, ulo, ilo, Qs, Bis, Bus, hyper_regs(A.h));
     __syncthreads();
-    strata_store_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
+    strata_store_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
     if constexpr (KERN != MF_RBF) {
         if (A.upd_user)
-            for (int t = threadIdx.x; t < nus; t += kStrataThreads) A.Bu[ulo + t] = Bus[t];
+            for (int t = threadIdx.x; t < nus; t += TH) A.Bu[ulo + t] = Bus[t];
     }
 }
 
@@ -524,11 +528,12 @@ constexpr int64_t kStrataSpinLimit = (int64_t)1 << 24;
 // checks occupancy, then launches cooperatively (hipLaunchCooperativeKernel:
 // the runtime refuses a grid that cannot be resident at once, and the epoch
 // then runs as one launch per stratum).
-template <typename T, int W, int GS, int V, int KERN, int S, int DEPTH = 1>
-__global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<T> A,
+template <typename T, int W, int GS, int V, int KERN, int S, int DEPTH = 1, int NW = kStrataWaves>
+__global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A,
                                                                     const int32_t* seq,
                                                                     int32_t n_seq, int32_t* done,
                                                                     int32_t* err) {
+    constexpr int TH = NW * kWave;
     extern __shared__ __align__(16) unsigned char smem[];
     __shared__ int s_abort;
     const int B = A.B;
@@ -538,7 +543,7 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<
     T* Bis = Qs + (size_t)nqi * A.k;
     T* Bus = Bis + nqi;
     const Hyper<T> h = hyper_regs(A.h);
-    strata_stage_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
+    strata_stage_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
     // probe: s_memrealtime (100 MHz) at wait start / wait end / block end /
     // signal, 4 stamps per (position t, workgroup w)
     auto stamp = [&](int t, int q) __attribute__((always_inline)) {
@@ -574,13 +579,13 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<
         if (s_abort) return;
         stamp(t, 1);
         // the user-bias slice is staged inside the block, behind its prologue
-        strata_block<T, W, GS, V, KERN, S, true, true, DEPTH>(A, (int64_t)s * B + w, ulo, ilo, Qs,
+        strata_block<T, W, GS, V, KERN, S, true, true, DEPTH, NW>(A, (int64_t)s * B + w, ulo, ilo, Qs,
                                                               Bis, Bus, h, nus);
         __syncthreads();
         stamp(t, 2);
         if constexpr (KERN != MF_RBF) {
             if (A.upd_user)
-                for (int x = threadIdx.x; x < nus; x += kStrataThreads)
+                for (int x = threadIdx.x; x < nus; x += TH)
                     __hip_atomic_store(A.Bu + ulo + x, Bus[x], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);     // write-through
         }
@@ -594,9 +599,9 @@ __global__ __launch_bounds__(kStrataThreads) void k_sgd_strata_epoch(StrataArgs<
     }
     __syncthreads();
     if (A.Dq)
-        strata_delta_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
+        strata_delta_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
     else
-        strata_store_slab<T, W, KERN>(A, ilo, nqi, Qs, Bis);
+        strata_store_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
 }
 
 // diagnostic: device buffer for the persistent kernel's phase stamps
@@ -622,22 +627,38 @@ inline size_t strata_ws_bytes(int32_t B, int32_t n_seq) {
 
 // Can all B workgroups of `kfn` be resident at once (the persistent kernel's
 // waits need it)?
-inline bool strata_coresident(const void* kfn, int B, size_t lds) {
+inline bool strata_coresident(const void* kfn, int B, size_t lds, int threads) {
     int dev = 0, cus = 0, per_cu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return false;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return false;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, kStrataThreads, lds) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, threads, lds) !=
         hipSuccess)
         return false;
     return (int64_t)cus * per_cu >= B;
 }
 
 // NS of the row layout (W, GS, V) that dispatch_rows picks for (k, dtype)
+// Workgroup sizes of the strata kernels: 16 waves (the default), and 8 waves
+// (FP32 only) for plans whose blocks are bound by the item degree rather
+// than by the slot count -- half the slots per step, half the per-step VALU
+// of a CU, about the same number of steps (C2: DESIGN.md section 5).
+// the 8-wave kernels exist for FP32 rows of one vector per lane (k <= 64)
+template <typename T, int V>
+constexpr bool strata_has_8_waves() {
+    return std::is_same<T, float>::value && V == 1;
+}
+
 template <typename T>
 struct StrataSlots {
+    int waves;
     template <int W, int GS, int V, int KERN>
-    int run() { return strata_slots<T, W, GS, V>(); }
+    int run() {
+        if (waves == 16) return strata_slots<T, W, GS, V, 16>();
+        if constexpr (strata_has_8_waves<T, V>())
+            if (waves == 8) return strata_slots<T, W, GS, V, 8>();
+        return -1;
+    }
 };
 
 template <typename T>
@@ -646,16 +667,20 @@ struct StrataRun {
 
     template <int W, int GS, int V, int KERN>
     int run() {
-        return go<W, GS, V, KERN, strata_group_slots<T, W, GS, V>()>();
+        constexpr int S = strata_group_slots<T, W, GS, V>();
+        if (p.n_slots == strata_slots<T, W, GS, V, 16>()) return go<W, GS, V, KERN, S, 16>();
+        if constexpr (strata_has_8_waves<T, V>()) {
+            if (p.n_slots == strata_slots<T, W, GS, V, 8>()) return go<W, GS, V, KERN, S, 8>();
+        }
+        set_error("plan has %d slots per step, the n_factors=%d layout needs %d (16 waves)%s",
+                  p.n_slots, p.k, strata_slots<T, W, GS, V, 16>(),
+                  strata_has_8_waves<T, V>() ? " or half that (8 waves)" : "");
+        return MF_ERR_INVALID;
     }
 
-    template <int W, int GS, int V, int KERN, int S>
+    template <int W, int GS, int V, int KERN, int S, int NW>
     int go() {
-        if (p.n_slots != strata_slots<T, W, GS, V>()) {
-            set_error("plan has %d slots per step, the n_factors=%d layout needs %d", p.n_slots,
-                      p.k, strata_slots<T, W, GS, V>());
-            return MF_ERR_INVALID;
-        }
+        constexpr int TH = NW * kWave;
         const size_t lds = strata_lds_bytes<T>(p.max_items, p.max_users, p.k);
         if (lds > (size_t)kLdsLimit) {
             set_error("strata block needs %zu B of LDS (> %d): use more blocks", lds, kLdsLimit);
@@ -665,7 +690,7 @@ struct StrataRun {
             set_error("the strata schedule needs n_factors >= 1");
             return MF_ERR_INVALID;
         }
-        auto kfn = k_sgd_strata<T, W, GS, V, KERN, S>;
+        auto kfn = k_sgd_strata<T, W, GS, V, KERN, S, NW>;
         MF_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         StrataArgs<T> a;
@@ -693,11 +718,13 @@ struct StrataRun {
         bool persistent = false;
         if ((p.flags & MF_FLAG_PERSISTENT) && p.ws &&
             p.ws_bytes >= strata_ws_bytes(p.B, p.n_seq) && a.p_bytes < (uint64_t)kBufDrop) {
-            auto efn = (p.flags & MF_FLAG_DEEP_PIPE) ? k_sgd_strata_epoch<T, W, GS, V, KERN, S, 2>
-                                                     : k_sgd_strata_epoch<T, W, GS, V, KERN, S, 1>;
+            // (the deep pipeline exists for 16 waves only)
+            auto efn = (NW == 16 && (p.flags & MF_FLAG_DEEP_PIPE))
+                           ? k_sgd_strata_epoch<T, W, GS, V, KERN, S, NW == 16 ? 2 : 1, NW>
+                           : k_sgd_strata_epoch<T, W, GS, V, KERN, S, 1, NW>;
             MF_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(efn),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            persistent = strata_coresident(reinterpret_cast<const void*>(efn), p.B, lds);
+            persistent = strata_coresident(reinterpret_cast<const void*>(efn), p.B, lds, TH);
             if (persistent) {
                 int32_t* done = static_cast<int32_t*>(p.ws);
                 int32_t* err = done + p.B;
@@ -707,7 +734,7 @@ struct StrataRun {
                 MF_HIP_CHECK(hipMemcpyAsync(err + 1, p.seq, sizeof(int32_t) * (size_t)p.n_seq,
                                             hipMemcpyHostToDevice, p.stream));
                 if (p.flags & MF_FLAG_NO_COOP) {
-                    hipLaunchKernelGGL(efn, dim3((unsigned)p.B), dim3(kStrataThreads), lds,
+                    hipLaunchKernelGGL(efn, dim3((unsigned)p.B), dim3(TH), lds,
                                        p.stream, a, dseq, nseq, done, err);
                 } else {
                     // cooperative: the runtime guarantees that all B workgroups
@@ -716,7 +743,7 @@ struct StrataRun {
                     void* kargs[] = {&a, &dseq, &nseq, &done, &err};
                     const hipError_t ce = hipLaunchCooperativeKernel(
                         reinterpret_cast<const void*>(efn), dim3((unsigned)p.B),
-                        dim3(kStrataThreads), kargs, (unsigned)lds, p.stream);
+                        dim3(TH), kargs, (unsigned)lds, p.stream);
                     if (ce != hipSuccess) {
                         (void)hipGetLastError();
                         persistent = false;
@@ -736,7 +763,7 @@ struct StrataRun {
             a.Dq = a.Dbi = nullptr;
             for (int32_t t = 0; t < p.n_seq; ++t) {
                 a.s = p.seq[t];
-                hipLaunchKernelGGL(kfn, dim3((unsigned)p.B), dim3(kStrataThreads), lds, p.stream,
+                hipLaunchKernelGGL(kfn, dim3((unsigned)p.B), dim3(TH), lds, p.stream,
                                    a);
             }
             if (p.dq) {

@@ -2,6 +2,8 @@
 // keep the best `amount` per user (recommender_base.py:214-271 scores all
 // candidate items with predict(bound_ratings=False) and sorts descending).
 //
+// amount <= 64 (recommend's default 10): k_topk_fused + k_topk_merge (below:
+// scores never leave the chip).  Larger amounts, or MF_TOPK_TWO_STAGE=1:
 // Stage 1 (k_topk_scores): one wave per (user, chunk of items); the user's
 //   factor row stays in registers, item rows stream from HBM/L2; each score
 //   becomes a 64-bit order-preserving key (1 = NaN); k_topk_exclude then
@@ -9,7 +11,9 @@
 // Stage 2 (k_topk_select): one workgroup per user: 8-pass radix select of
 //   the amount-th key (LDS histograms), collect, bitonic sort in LDS by
 //   (score desc, item id asc).
+#include <algorithm>
 #include <climits>
+#include <cstdlib>
 
 #include "mf_common.hpp"
 
@@ -226,6 +230,244 @@ __global__ __launch_bounds__(kBlock) void k_topk_select(const uint64_t* __restri
     }
 }
 
+// ---------------------------------------------------------------- fused
+// k_topk_fused: the same scores (k_read's arithmetic: lane partials of the
+// scalar layout, group_sum<GS>, predict_one) without materialising them.
+// Workgroup (split x, user block y) scores items [ibeg, iend) of its split
+// against kFusedUsers users whose rows sit in registers; every wave walks
+// one item at a time.  A score enters the user's LDS candidate list only if
+// it beats the list's current threshold (the amount-th best so far, in the
+// order (score desc, item id asc)); excluded items are looked up (binary
+// search in the user's sorted CSR list) only for such candidates.  After
+// every chunk of items a barrier; lists that grew past A2 + chunk are
+// bitonic-sorted and cut to the best A2 (A2 = amount rounded up to a power
+// of two), raising the threshold.  At the end each list is sorted and its
+// best `amount` go to the split's partial output; k_topk_merge merges the
+// splits per user.  Random scores settle the threshold after a few chunks,
+// so almost every score costs its reduction and one compare.
+constexpr int kFusedUsers = 16;          // users per workgroup (registers)
+constexpr int kFusedMaxAmount = 64;
+constexpr int kFusedItemsPerWave = 16;   // items per wave between barriers
+constexpr int kFusedChunk = kWavesPerBlock * kFusedItemsPerWave;
+constexpr int kFusedCap = 256;           // list capacity: A2 + 2 chunks <= 256
+
+struct Cand { uint64_t key; int32_t id; };
+
+// (key desc, id asc): does (ka, ia) come before (kb, ib)?
+__device__ __forceinline__ bool cand_before(uint64_t ka, int32_t ia, uint64_t kb, int32_t ib) {
+    return ka > kb || (ka == kb && ia < ib);
+}
+
+// bitonic sort of n (power of two) candidates in LDS by the whole workgroup
+// subset `lanes` (threads t < lanes participate; all threads hit the barriers)
+__device__ __forceinline__ void cand_sort(uint64_t* key, int32_t* id, int n, int t, int lanes) {
+    for (int sz = 2; sz <= n; sz <<= 1) {
+        for (int st = sz >> 1; st > 0; st >>= 1) {
+            for (int x = t; x < n && t < lanes; x += lanes) {
+                const int y = x ^ st;
+                if (y > x) {
+                    const bool desc = (x & sz) == 0;
+                    const uint64_t kx = key[x], ky = key[y];
+                    const int32_t ix = id[x], iy = id[y];
+                    const bool xfirst = cand_before(kx, ix, ky, iy);
+                    if (desc ? !xfirst : xfirst) {
+                        key[x] = ky; key[y] = kx;
+                        id[x] = iy; id[y] = ix;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ __forceinline__ bool excluded(const int64_t* ptr, const int32_t* items, int qy,
+                                         int32_t it) {
+    if (!ptr) return false;
+    int64_t lo = ptr[qy], hi = ptr[qy + 1];          // sorted ascending
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int32_t v = items[mid];
+        if (v == it) return true;
+        if (v < it) lo = mid + 1;
+        else hi = mid;
+    }
+    return false;
+}
+
+template <typename T>
+struct FusedArgs {
+    const int32_t* users; int32_t nq;
+    const T* P; const T* Q; const T* Bu; const T* Bi;
+    int32_t n_items, k, amount, a2, n_splits;
+    Hyper<T> h;
+    const int64_t* ex_ptr; const int32_t* ex_items;
+    uint64_t* part_key; int32_t* part_id;           // [nq][n_splits][amount]
+};
+
+template <typename T, int GS, int V, int KERN>
+__global__ __launch_bounds__(kBlock) void k_topk_fused(FusedArgs<T> A) {
+    static_assert(GS == kWave || V == 1, "the scalar layout: one item per wave");
+    __shared__ uint64_t s_key[kFusedUsers][kFusedCap];
+    __shared__ int32_t s_id[kFusedUsers][kFusedCap];
+    __shared__ int s_cnt[kFusedUsers];
+    __shared__ uint64_t s_tk[kFusedUsers];
+    __shared__ int32_t s_ti[kFusedUsers];
+    constexpr int R = kWave / GS;                    // items per wave instruction
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    const int g = lane / GS, l = lane % GS;
+    const int split = blockIdx.x, q0 = blockIdx.y * kFusedUsers;
+    const int k = A.k;
+    const int64_t span = ((int64_t)A.n_items + A.n_splits - 1) / A.n_splits;
+    const int ibeg = (int)min((int64_t)A.n_items, span * split);
+    const int iend = (int)min((int64_t)A.n_items, span * (split + 1));
+    if (tid < kFusedUsers) {
+        s_cnt[tid] = 0;
+        s_tk[tid] = 0ull;                            // below every candidate key (>= 1)
+        s_ti[tid] = 0x7fffffff;
+    }
+    T p[kFusedUsers][V], bu[kFusedUsers];
+#pragma unroll
+    for (int x = 0; x < kFusedUsers; ++x) {
+        const int qy = q0 + x;
+        const int32_t uu = qy < A.nq ? A.users[qy] : -1;
+        const bool uk = uu >= 0;
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            const int f = l + v * GS;
+            p[x][v] = (uk && f < k) ? A.P[(int64_t)uu * k + f] : (T)0;
+        }
+        bu[x] = (uk && KERN != MF_RBF) ? A.Bu[uu] : (T)0;
+    }
+    __syncthreads();
+    for (int c0 = ibeg; c0 < iend; c0 += kFusedChunk) {
+        // thresholds of this chunk (wave-uniform copies)
+        uint64_t tk[kFusedUsers];
+        int32_t ti[kFusedUsers];
+#pragma unroll
+        for (int x = 0; x < kFusedUsers; ++x) { tk[x] = s_tk[x]; ti[x] = s_ti[x]; }
+        for (int j = 0; j < kFusedItemsPerWave; j += R) {
+            const int it = c0 + wv * kFusedItemsPerWave + j + g;
+            const bool have = it < iend;
+            const T* qr = A.Q + (int64_t)(have ? it : 0) * k;
+            T q[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const int f = l + v * GS;
+                q[v] = (have && f < k) ? qr[f] : (T)0;
+            }
+            const T bi = (have && KERN != MF_RBF) ? A.Bi[it] : (T)0;
+#pragma unroll
+            for (int x = 0; x < kFusedUsers; ++x) {
+                T sc = (T)0;
+#pragma unroll
+                for (int v = 0; v < V; ++v) {
+                    if constexpr (KERN == MF_RBF) {
+                        const T d = p[x][v] - q[v];
+                        sc = sc + d * d;
+                    } else {
+                        sc = sc + p[x][v] * q[v];
+                    }
+                }
+                sc = group_sum<GS>(sc);
+                T pred;                                  // predict_one (mf_rows.hpp)
+                if constexpr (KERN == MF_LINEAR) pred = ((A.h.mu + bi) + bu[x]) + sc;
+                else if constexpr (KERN == MF_SIGMOID)
+                    pred = A.h.a + A.h.c * ((T)1 / ((T)1 + dexp<T>(-(((A.h.mu + bu[x]) + bi) + sc))));
+                else pred = A.h.a + A.h.c * dexp<T>((-A.h.gamma) * sc);
+                const uint64_t key = order_key((double)pred);
+                const int qy = q0 + x;
+                if (have && l == 0 && qy < A.nq && cand_before(key, it, tk[x], ti[x]) &&
+                    !excluded(A.ex_ptr, A.ex_items, qy, it)) {
+                    const int slot = atomicAdd(&s_cnt[x], 1);
+                    s_key[x][slot] = key;
+                    s_id[x][slot] = it;
+                }
+            }
+        }
+        __syncthreads();
+        // cut lists that can no longer take a full chunk
+#pragma unroll 1
+        for (int x = 0; x < kFusedUsers; ++x) {
+            const int n = s_cnt[x];
+            if (n <= A.a2 + kFusedChunk) continue;       // uniform: s_cnt read after the barrier
+            int n2 = 1;
+            while (n2 < n) n2 <<= 1;
+            for (int y = n + tid; y < n2; y += kBlock) { s_key[x][y] = 0ull; s_id[x][y] = 0x7fffffff; }
+            __syncthreads();
+            cand_sort(s_key[x], s_id[x], n2, tid, kBlock);
+            if (tid == 0) {
+                s_cnt[x] = A.a2;
+                s_tk[x] = s_key[x][A.amount - 1];        // the amount-th best so far
+                s_ti[x] = s_id[x][A.amount - 1];
+            }
+            __syncthreads();
+        }
+    }
+    // final: sort each list, write its best `amount` (padding: key 0, id -1)
+#pragma unroll 1
+    for (int x = 0; x < kFusedUsers; ++x) {
+        const int qy = q0 + x;
+        if (qy >= A.nq) break;                           // uniform
+        const int n = s_cnt[x];
+        int n2 = 1;
+        while (n2 < max(n, A.a2)) n2 <<= 1;
+        for (int y = n + tid; y < n2; y += kBlock) { s_key[x][y] = 0ull; s_id[x][y] = 0x7fffffff; }
+        __syncthreads();
+        cand_sort(s_key[x], s_id[x], n2, tid, kBlock);
+        for (int y = tid; y < A.amount; y += kBlock) {
+            const int64_t o = ((int64_t)qy * A.n_splits + split) * A.amount + y;
+            const bool ok = y < n;
+            A.part_key[o] = ok ? s_key[x][y] : 0ull;
+            A.part_id[o] = ok ? s_id[x][y] : -1;
+        }
+        __syncthreads();
+    }
+}
+
+// merge the n_splits partial lists of one user (a workgroup per user)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_topk_merge(const uint64_t* __restrict__ part_key,
+                                                       const int32_t* __restrict__ part_id,
+                                                       int32_t n_splits, int32_t amount,
+                                                       int32_t* out_items, T* out_scores) {
+    __shared__ uint64_t s_key[kFusedCap * 4];
+    __shared__ int32_t s_id[kFusedCap * 4];
+    const int qy = blockIdx.x, tid = threadIdx.x;
+    const int n = n_splits * amount;                     // <= 4 * kFusedCap (launcher)
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    for (int y = tid; y < n2; y += kBlock) {
+        const bool ok = y < n;
+        const int64_t o = (int64_t)qy * n + y;
+        const int32_t id = ok ? part_id[o] : -1;
+        s_key[y] = (ok && id >= 0) ? part_key[o] : 0ull;
+        s_id[y] = (ok && id >= 0) ? id : 0x7fffffff;
+    }
+    __syncthreads();
+    cand_sort(s_key, s_id, n2, tid, kBlock);
+    for (int y = tid; y < amount; y += kBlock) {
+        const bool ok = s_key[y] != 0ull;
+        out_items[(int64_t)qy * amount + y] = ok ? s_id[y] : -1;
+        out_scores[(int64_t)qy * amount + y] =
+            ok ? (T)key_score(s_key[y]) : (T)__longlong_as_double(0x7ff8000000000000LL);
+    }
+}
+
+// splits of the item range for the fused path: enough workgroups to fill the
+// chip (~6 per CU), at least 512 items per split, n_splits * amount <= 1024
+inline int topk_splits(int32_t nq, int32_t n_items, int32_t amount) {
+    const int64_t blocks_q = ((int64_t)nq + kFusedUsers - 1) / kFusedUsers;
+    int64_t s = (1536 + blocks_q - 1) / blocks_q;
+    s = std::min<int64_t>(s, std::max<int64_t>(1, n_items / 512));
+    s = std::min<int64_t>(s, 1024 / std::max(amount, 1));
+    return (int)std::max<int64_t>(1, s);
+}
+inline bool topk_fused(int32_t amount) {
+    const char* e = std::getenv("MF_TOPK_TWO_STAGE");
+    return amount <= kFusedMaxAmount && !(e && std::atoi(e) == 1);
+}
+
 struct TopkLaunch {
     const int32_t* users; int32_t nq; double mu; const void* bu; const void* bi;
     const void* P; const void* Q; int32_t n_items; int32_t k; double gamma, lo, hi;
@@ -234,6 +476,29 @@ struct TopkLaunch {
 
     template <typename T, int GS, int V, int KERN>
     int run() {
+        if (topk_fused(amount)) {
+            FusedArgs<T> f;
+            f.users = users; f.nq = nq; f.P = (const T*)P; f.Q = (const T*)Q;
+            f.Bu = (const T*)bu; f.Bi = (const T*)bi; f.n_items = n_items; f.k = k;
+            f.amount = amount;
+            int a2 = 1;
+            while (a2 < amount) a2 <<= 1;
+            f.a2 = a2;
+            f.n_splits = topk_splits(nq, n_items, amount);
+            f.h = make_hyper<T>(mu, 0.0, 0.0, gamma, lo, hi);
+            f.ex_ptr = ex_items ? ex_ptr : nullptr; f.ex_items = ex_items;
+            const size_t np = (size_t)nq * f.n_splits * amount;
+            f.part_key = (uint64_t*)ws;
+            f.part_id = (int32_t*)((uint64_t*)ws + np);
+            const unsigned by = (unsigned)((nq + kFusedUsers - 1) / kFusedUsers);
+            hipLaunchKernelGGL((k_topk_fused<T, GS, V, KERN>), dim3((unsigned)f.n_splits, by),
+                               dim3(kBlock), 0, stream, f);
+            hipLaunchKernelGGL(k_topk_merge<T>, dim3((unsigned)nq), dim3(kBlock), 0, stream,
+                               (const uint64_t*)f.part_key, (const int32_t*)f.part_id, f.n_splits,
+                               amount, out_items, (T*)out_scores);
+            MF_HIP_CHECK(hipGetLastError());
+            return MF_OK;
+        }
         TopkArgs<T> a;
         a.users = users; a.P = (const T*)P; a.Q = (const T*)Q;
         a.Bu = (const T*)bu; a.Bi = (const T*)bi;
@@ -262,8 +527,10 @@ struct TopkLaunch {
 using namespace mf;
 
 extern "C" size_t mf_topk_workspace_bytes(int32_t n_query, int32_t n_items, int32_t amount) {
-    (void)amount;
     if (n_query <= 0 || n_items <= 0) return 0;
+    if (topk_fused(amount))       // partial lists: n_query x splits x amount (key + id)
+        return (sizeof(uint64_t) + sizeof(int32_t)) * (size_t)n_query *
+               (size_t)topk_splits(n_query, n_items, amount) * (size_t)std::max(amount, 1);
     return sizeof(uint64_t) * (size_t)n_query * (size_t)n_items;
 }
 

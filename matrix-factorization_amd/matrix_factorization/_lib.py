@@ -65,6 +65,7 @@ SIGNATURES = {
     "mf_strata_lds_bytes": (ctypes.c_size_t, [_I32, _I32, _I32, _I32]),
     "mf_strata_lds_limit": (ctypes.c_int32, []),
     "mf_strata_slots": (ctypes.c_int32, [_I32, _I32]),
+    "mf_strata_slots_waves": (ctypes.c_int32, [_I32, _I32, _I32]),
     "mf_sse_workspace_bytes": (ctypes.c_size_t, [_I64]),
     "mf_sse": (ctypes.c_int, [
         _P, _P, _P, _I64, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F64,

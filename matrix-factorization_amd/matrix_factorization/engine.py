@@ -239,10 +239,15 @@ def sched_strata(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int, n_blo
     return sched[:npos], bstep
 
 
-def strata_slots(k: int, dcode: int) -> int:
-    ns = int(_lib.load().mf_strata_slots(k, dcode))
+def strata_slots(k: int, dcode: int, waves: int = 16) -> int:
+    """Rating slots per step of the strata kernel with ``waves`` waves per
+    workgroup (16, or 8 for FP32 rows of k <= 64); 0 if that kernel does not
+    exist."""
+    ns = int(_lib.load().mf_strata_slots_waves(k, dcode, waves))
     if ns <= 0:
-        _lib.check(1, "mf_strata_slots")
+        if waves == 16:
+            _lib.check(1, "mf_strata_slots")
+        return 0
     return ns
 
 
@@ -266,6 +271,15 @@ def choose_strata_blocks(u, i, n_users, n_items, k, dcode, max_blocks=None):
         if B >= max(n_items, 1) and B >= max(n_users, 1):
             raise ValueError("strata schedule: a single item row does not fit in LDS")
         B = int(np.ceil(B * 1.25)) + 1
+
+
+def _under_rocprofiler() -> bool:
+    """True inside `rocprofv3 ... -- python ...`: its dispatch interception
+    (ROCm 7.x) segfaults on hipLaunchCooperativeKernel, so profiled runs
+    launch the persistent strata kernel plainly (same kernel; the occupancy
+    check stays the co-residency guard)."""
+    return ("rocprofiler" in os.environ.get("LD_PRELOAD", "")
+            or any(k.startswith("ROCPROF") for k in os.environ))
 
 
 def default_sgd_flags() -> int:
@@ -397,10 +411,18 @@ class SGDEngine:
         self.colored = offs
         return len(offs) - 1
 
-    def prepare_strata(self, n_blocks: Optional[int] = None) -> "StrataPlan":
+    def prepare_strata(self, n_blocks: Optional[int] = None,
+                       waves: Optional[int] = None) -> "StrataPlan":
         """Build the stratified plan once and store a padded copy of the
         ratings in plan order (block-major, step-major, slot-minor).  The
-        host arrays keep the original rating order."""
+        host arrays keep the original rating order.
+
+        ``waves``: workgroup size of the strata kernels, 16 or 8 (FP32,
+        k <= 64).  None = by the plan: when the 16-wave plan fills fewer
+        than 70 % of its slots (steps bound by the item degree of the
+        blocks, not by the slot count), the 8-wave plan is built too and
+        kept if steps * waves -- the per-CU VALU issue of an epoch, which
+        bounds such plans (PMC) -- is lower."""
         if self.colored is not None or self.strata is not None:
             raise RuntimeError("ratings already permuted by another schedule")
         if n_blocks is None:
@@ -410,9 +432,26 @@ class SGDEngine:
             B = int(n_blocks)
             ub = balanced_bounds(self.u_host, self.n_users, B)
             ib = balanced_bounds(self.i_host, self.n_items, B)
-        ns = strata_slots(self.k, self.dcode)
-        sched, bstep = sched_strata(self.u_host, self.i_host, self.n_users, self.n_items, B,
-                                    ub, ib, ns)
+        env = os.environ.get("MF_STRATA_WAVES")
+        if waves is None and env in ("8", "16"):
+            waves = int(env)
+        cand = [waves] if waves is not None else [16, 8]
+        best = None
+        for wv in cand:
+            ns = strata_slots(self.k, self.dcode, wv)
+            if ns <= 0:
+                if waves is not None:
+                    raise ValueError(f"no {wv}-wave strata kernel for n_factors={self.k}, "
+                                     f"dtype={self.dtype}")
+                continue
+            sched, bstep = sched_strata(self.u_host, self.i_host, self.n_users, self.n_items, B,
+                                        ub, ib, ns)
+            cost = int(bstep[-1]) * wv
+            if best is None or cost < best[0]:
+                best = (cost, ns, sched, bstep)
+            if waves is None and wv == 16 and self.n / max(len(sched), 1) >= 0.7:
+                break                       # well filled: the 16-wave plan it is
+        _, ns, sched, bstep = best
         plan = StrataPlan(B, ns, ub, ib, bstep, sched)
         plan.to_device(self.u, self.i, self.r, self.dev)
         self.strata = plan
@@ -451,7 +490,7 @@ class SGDEngine:
         flags = _lib.MF_FLAG_PERSISTENT if persistent else 0
         if persistent and self._deep_pipe(pl):
             flags |= _lib.MF_FLAG_DEEP_PIPE
-        if os.environ.get("MF_STRATA_COOP") == "0":
+        if os.environ.get("MF_STRATA_COOP") == "0" or _under_rocprofiler():
             flags |= _lib.MF_FLAG_NO_COOP
         wsb = int(_lib.load().mf_strata_workspace_bytes(pl.B, len(seq)))
         old = getattr(self, "_strata_ws", None)
@@ -634,54 +673,81 @@ class SGDEngine:
                           self.max_rating, int(bound), _tp(out), self.stream)
         return out.cpu().numpy().astype(np.float64)
 
-    # score keys of one top-k launch: n_query * n_items * 8 B; users beyond
-    # this budget go in further launches
+    # workspace of one top-k launch (fused path: the partial lists; two-stage
+    # path, amount > 64: n_query * n_items * 8 B of keys); users beyond this
+    # budget go in further launches
     topk_ws_budget = 1 << 30
+
+    def topk_prepare(self, users: np.ndarray, amount: int,
+                     ex_ptr: Optional[np.ndarray] = None,
+                     ex_items: Optional[np.ndarray] = None) -> dict:
+        """Device-resident top-k batch: query ids, exclusion CSR (each user's
+        list sorted, as the fused kernel binary-searches it), workspace and
+        outputs, and the users per launch (``topk_ws_budget``)."""
+        if self.bias_only:
+            raise NotImplementedError("top-k is implemented for factor models")
+        users = np.ascontiguousarray(users, np.int32)
+        nq = len(users)
+        q = {"nq": nq, "amount": int(amount)}
+        if nq == 0 or amount == 0:
+            return q
+        to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev)  # noqa: E731
+        q["users"] = to(users)
+        q["ex_ptr"] = q["ex_items"] = None
+        if ex_ptr is not None:
+            ex_ptr = np.ascontiguousarray(ex_ptr, np.int64)
+            ex_items = np.ascontiguousarray(ex_items, np.int32)
+            if len(ex_ptr) != nq + 1:
+                raise ValueError("ex_ptr needs n_query + 1 offsets")
+            seg = np.repeat(np.arange(nq, dtype=np.int64), np.diff(ex_ptr))
+            ex_items = ex_items[np.lexsort((ex_items, seg))]
+            q["ex_ptr"] = to(ex_ptr - ex_ptr[0])
+            q["ex_items"] = to(ex_items if len(ex_items) else np.zeros(1, np.int32))
+        lib = _lib.load()
+        # users per launch: grid limits, then halve until the workspace fits
+        chunk = min(nq, 65535 if amount > 64 else 1 << 20)
+        while chunk > 1 and lib.mf_topk_workspace_bytes(chunk, self.n_items,
+                                                        amount) > self.topk_ws_budget:
+            chunk = (chunk + 1) // 2
+        q["chunk"] = chunk
+        wsb = lib.mf_topk_workspace_bytes(chunk, self.n_items, amount)
+        q["ws"] = torch.empty(max(wsb, 8), dtype=torch.uint8, device=self.dev)
+        q["items"] = torch.empty((nq, amount), dtype=torch.int32, device=self.dev)
+        q["scores"] = torch.empty((nq, amount), dtype=self.tdt, device=self.dev)
+        return q
+
+    def topk_launch(self, q: dict) -> None:
+        """Enqueue mf_topk for a prepared batch (results stay on the device)."""
+        nq, amount = q["nq"], q["amount"]
+        if nq == 0 or amount == 0:
+            return
+        chunk = q["chunk"]
+        es_i, es_s = q["items"].element_size(), q["scores"].element_size()
+        with torch.cuda.device(self.dev):
+            for q0 in range(0, nq, chunk):
+                q1 = min(nq, q0 + chunk)
+                # CSR offsets stay absolute: the chunk's ptr array starts at row q0
+                dp = None if q["ex_ptr"] is None else _VOID(q["ex_ptr"].data_ptr() + 8 * q0)
+                _lib.call("mf_topk", _VOID(q["users"].data_ptr() + 4 * q0), q1 - q0,
+                          self.global_mean, _tp(self.bu), _tp(self.bi), _tp(self.P),
+                          _tp(self.Q), self.n_items, self.k, self.kcode, self.dcode,
+                          self.gamma, self.min_rating, self.max_rating, dp,
+                          _tp(q["ex_items"]), amount, _tp(q["ws"]),
+                          _VOID(q["items"].data_ptr() + es_i * amount * q0),
+                          _VOID(q["scores"].data_ptr() + es_s * amount * q0), self.stream)
 
     def topk(self, users: np.ndarray, amount: int, ex_ptr: Optional[np.ndarray] = None,
              ex_items: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
         """Best ``amount`` items per internal user id: (item ids, scores).
 
         ``ex_ptr`` / ``ex_items``: optional CSR exclusions (query q skips
-        items ex_items[ex_ptr[q]:ex_ptr[q+1]]).  Users are processed in
-        chunks whose score workspace fits ``topk_ws_budget``."""
-        if self.bias_only:
-            raise NotImplementedError("top-k is implemented for factor models")
-        users = np.ascontiguousarray(users, np.int32)
-        nq = len(users)
-        items_out = np.full((nq, amount), -1, np.int32)
-        scores_out = np.full((nq, amount), np.nan, np.float64)
-        if nq == 0 or amount == 0:
-            return items_out, scores_out
-        if ex_ptr is not None:
-            ex_ptr = np.ascontiguousarray(ex_ptr, np.int64)
-            ex_items = np.ascontiguousarray(ex_items, np.int32)
-            if len(ex_ptr) != nq + 1:
-                raise ValueError("ex_ptr needs n_query + 1 offsets")
-        lib = _lib.load()
-        chunk = int(max(1, min(65535, self.topk_ws_budget // max(8 * self.n_items, 1), nq)))
-        wsb = lib.mf_topk_workspace_bytes(chunk, self.n_items, amount)
-        ws = torch.empty(max(wsb, 8), dtype=torch.uint8, device=self.dev)
-        d_items = torch.empty((chunk, amount), dtype=torch.int32, device=self.dev)
-        d_scores = torch.empty((chunk, amount), dtype=self.tdt, device=self.dev)
-        for q0 in range(0, nq, chunk):
-            q1 = min(nq, q0 + chunk)
-            ud = torch.from_numpy(users[q0:q1]).to(self.dev)
-            dp = di = None
-            if ex_ptr is not None:
-                lo, hi = int(ex_ptr[q0]), int(ex_ptr[q1])
-                dp = torch.from_numpy(ex_ptr[q0:q1 + 1] - lo).to(self.dev)
-                di = torch.from_numpy(ex_items[lo:hi] if hi > lo else
-                                      np.zeros(1, np.int32)).to(self.dev)
-            with torch.cuda.device(self.dev):
-                _lib.call("mf_topk", _tp(ud), q1 - q0, self.global_mean, _tp(self.bu),
-                          _tp(self.bi), _tp(self.P), _tp(self.Q), self.n_items, self.k,
-                          self.kcode, self.dcode, self.gamma, self.min_rating,
-                          self.max_rating, _tp(dp), _tp(di), amount, _tp(ws), _tp(d_items),
-                          _tp(d_scores), self.stream)
-            items_out[q0:q1] = d_items[: q1 - q0].cpu().numpy()
-            scores_out[q0:q1] = d_scores[: q1 - q0].cpu().numpy()
-        return items_out, scores_out
+        items ex_items[ex_ptr[q]:ex_ptr[q+1]])."""
+        q = self.topk_prepare(users, amount, ex_ptr, ex_items)
+        if q["nq"] == 0 or amount == 0:
+            return (np.full((q["nq"], amount), -1, np.int32),
+                    np.full((q["nq"], amount), np.nan, np.float64))
+        self.topk_launch(q)
+        return q["items"].cpu().numpy(), q["scores"].cpu().numpy().astype(np.float64)
 
 
 class BiasALS:

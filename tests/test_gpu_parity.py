@@ -247,7 +247,8 @@ def test_topk_ties_and_chunking(mf):
     users = list(d["rec_users"]) + [d["rec_users"][0]]
     one = m.recommend_batch(users, amount=40, bound_ratings=False)
     eng = m._predictor()
-    eng.topk_ws_budget = 8 * m.n_items * 2          # two users per launch
+    lib = mf._lib.load()
+    eng.topk_ws_budget = lib.mf_topk_workspace_bytes(2, m.n_items, 40)   # two users per launch
     try:
         many = m.recommend_batch(users, amount=40, bound_ratings=False)
     finally:
@@ -261,6 +262,30 @@ def test_topk_ties_and_chunking(mf):
         assert len(g) == 40 * users.count(user)
         assert g["item_id"].tolist()[:40] == ref["item_id"].tolist()
         assert np.array_equal(g["rating_pred"].to_numpy()[:40], ref["rating_pred"].to_numpy())
+
+
+@pytest.mark.parametrize("amount", [1, 10, 64])
+def test_topk_fused_equals_two_stage(mf, amount, monkeypatch):
+    """k_topk_fused + k_topk_merge (scores never materialised) return exactly
+    what the two-stage path (all keys in HBM, radix select) returns: same
+    ids, same scores, exclusions applied, for a batch large enough to split
+    the item range across workgroups."""
+    d = load_golden("c1_linear")
+    hp = golden_hp(d)
+    hp.update(n_epochs=2, verbose=0)
+    X, y = _frame(d)
+    np.random.seed(int(d["seed"]))
+    m = mf.KernelMF(**hp).fit(X, y)
+    users = list(m.user_id_map)[:300]
+    known = X.assign(r=y)
+    known = known[known.user_id.isin(users[::3])]
+    fused = m.recommend_batch(users, amount=amount, exclude_known=known, bound_ratings=False)
+    monkeypatch.setenv("MF_TOPK_TWO_STAGE", "1")
+    two = m.recommend_batch(users, amount=amount, exclude_known=known, bound_ratings=False)
+    pd.testing.assert_frame_equal(fused, two)
+    assert len(fused) == amount * len(users)
+    pairs = set(zip(known.user_id, known.item_id))
+    assert not any((u, i) in pairs for u, i in zip(fused.user_id, fused.item_id))
 
 
 def test_predict_sees_in_place_edits(mf):

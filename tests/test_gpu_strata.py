@@ -198,3 +198,67 @@ def test_deep_pipe_equals_per_stratum_launches(dtype, B, kernel, k, nu, ni):
         out.append(eng.params_numpy())
     for a, b in zip(*out):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("kernel,k", [("sigmoid", 32), ("linear", 64), ("rbf", 16)])
+def test_eight_wave_kernels(kernel, k):
+    """The 8-wave strata kernels (plans of half the slots, FP32, k <= 64):
+    the persistent epoch is bit-identical to per-stratum launches, and both
+    are the oracle's sequential sweep in the plan's serial order (FP32 vs
+    FP64: train RMSE within 1e-5)."""
+    import oracle
+
+    nu, ni, nnz = 3000, 800, 120000
+    u, i, r = _synthetic(71, nu, ni, nnz)
+    rs = np.random.RandomState(72)
+    P = rs.normal(0, 0.1, (nu, k)); Q = rs.normal(0, 0.1, (ni, k))
+    bu = rs.normal(0, 0.1, nu); bi = rs.normal(0, 0.1, ni)
+    out = []
+    for persistent in (True, False):
+        eng = _engine(u, i, r, nu, ni, k, kernel, "float32", P, Q, bu, bi)
+        plan = eng.prepare_strata(n_blocks=6, waves=8)
+        from matrix_factorization.engine import strata_slots
+        assert plan.NS == strata_slots(k, eng.dcode, 8) == strata_slots(k, eng.dcode) // 2
+        orders = []
+        for ep in range(2):
+            seq = np.random.RandomState(ep).permutation(6).astype(np.int32)
+            _, n_launch = eng.epoch_strata(seq, 3000 + ep, lr=0.01, reg=0.02, timing=True,
+                                           persistent=persistent)
+            assert n_launch == (1 if persistent else 6)
+            orders.append(plan.serial_order(seq, 3000 + ep))
+        eng.check_strata()
+        eng.sse_async(0)
+        out.append(eng.params_numpy() + (eng.rmse_values(1)[0],))
+    for a, b in zip(out[0][:4], out[1][:4]):
+        assert np.array_equal(a, b)
+    P2, Q2, bu2, bi2 = P.copy(), Q.copy(), bu.copy(), bi.copy()
+    hyp = dict(kernel=kernel, gamma=1.0 / k, min_rating=1.0, max_rating=5.0)
+    for order in orders:
+        oracle.sgd_pass(eng.u_host, eng.i_host, eng.r_host.astype(np.float64), eng.global_mean,
+                        bu2, bi2, P2, Q2, lr=0.01, reg=0.02, order=order, **hyp)
+    ro = oracle.rmse(eng.u_host, eng.i_host, eng.r_host.astype(np.float64), eng.global_mean,
+                     bu2, bi2, P2, Q2, **hyp)
+    assert abs(out[0][4] - ro) < 1e-5
+
+
+def test_auto_waves_picks_lower_cost():
+    """prepare_strata(waves=None) keeps the 16-wave plan when it fills >= 70 %
+    of its slots, else the plan with the lower steps x waves (the per-CU
+    VALU issue that bounds item-degree-bound plans)."""
+    from matrix_factorization.engine import strata_slots
+
+    nu, ni, k, B = 20000, 400, 32, 4
+    u, i, r = _synthetic(81, nu, ni, 200000)
+    rs = np.random.RandomState(82)
+    P, Q = rs.normal(0, 0.1, (nu, k)), rs.normal(0, 0.1, (ni, k))
+    plans = {}
+    for wv in (16, 8, None):
+        eng = _engine(u, i, r, nu, ni, k, "sigmoid", "float32", P, Q, np.zeros(nu), np.zeros(ni))
+        plans[wv] = eng.prepare_strata(n_blocks=B, waves=wv)
+    cost = {wv: int(plans[wv].bstep[-1]) * wv for wv in (16, 8)}
+    fill16 = len(u) / plans[16].n_positions
+    expect = 16 if fill16 >= 0.7 else min(cost, key=cost.get)
+    assert plans[None].NS == strata_slots(k, eng.dcode, expect), (fill16, cost)
+    seq = np.random.RandomState(0).permutation(B).astype(np.int32)
+    eng.epoch_strata(seq, 5, 0.01, 0.02)
+    eng.check_strata()
