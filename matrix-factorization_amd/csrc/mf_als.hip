@@ -26,6 +26,8 @@
 //      wave 0: b_e = (sum t - s'.D^-1 f') / (n + reg - s'.D^-1 s'),
 //      w_e = U^-1 D^-1 (f' - b_e s')   (f' = U^-T f, s' = U^-T s).
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <utility>
 
 #include "mf_common.hpp"
@@ -37,6 +39,7 @@ constexpr int kAlsChunk = 64;        // other-side rows per LDS chunk (32 K-step
 constexpr int kAlsMaxFactors = 128;
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
 
 // MFMA tiles of the symmetric Gramian: column blocks J = 0..NT-1, row blocks
 // I <= J.  Tile q is computed by wave q % 4.  The two right-hand columns
@@ -429,6 +432,379 @@ __global__ __launch_bounds__(kAlsThreads, 2) void k_als_solve(AlsArgs A) {
     als_stamp(A, 3);
 }
 
+// ---- one wave per entity ---------------------------------------------------
+//
+// k_als_wave: the same system, solved by ONE wave with no cross-wave
+// synchronisation (one-wave workgroups; at rank 128 four per CU, one per
+// SIMD):
+//   1. Gramian, fed by an all-DMA pipeline (nothing the loop consumes is a
+//      VMEM register load, so no vmcnt(0) drain): per chunk of kAlsRingRows
+//      rows, stage A moves the ids and ratings (global_load_lds, 4 B per
+//      lane) into LDS slots four chunks ahead; stage B, two chunks ahead,
+//      reads the ids back and moves the rows (16 B per lane, 1 KiB = 8 / NT
+//      rows per wave-instruction) into a 3-chunk ring and the other side's
+//      biases into their slot; counted vmcnt waits + the (one-wave) barrier
+//      order them for the ds_reads.  Lane (c, h) of K-step s reads column
+//      32 I + c of chunk row 2 s + h, which is both the A and the B operand
+//      of tile (I, J); every upper tile of the KP x KP Gramian accumulates
+//      in the wave's own registers.  The right-hand columns (sum t z, sum z)
+//      on the VALU beside the MFMAs.
+//   2. symmetric elimination in registers.  Pivot j's row is extracted from
+//      its tile register (wave-uniform dynamic index), swapped across the
+//      lane halves (v_permlane32_swap) and readlane'd for the pivot; its
+//      values at a lane's columns come from registers, the multipliers of a
+//      lane's rows from the row published in LDS (zeros at columns <= j).
+//      The row of pivot j + 1 is extracted and published as soon as its own
+//      tile row is updated, so that LDS round trip overlaps the rest of
+//      pivot j's update.  The two right-hand columns live row-per-lane
+//      (rows L, L + 64).  The eliminated rows (D U) go to LDS packed.
+//   3. the bias border (Schur complement) and the back substitution, as in
+//      k_als_solve.
+// Ranks with n_factors % 4 != 0 (rows not 16-byte aligned for the DMA) use
+// k_als_solve.
+constexpr int kAlsRingRows = 16;       // rows per ring chunk (8 K-steps)
+constexpr int kAlsRowBufs = 3;         // ring chunks (rows two chunks ahead)
+constexpr int kAlsIdSlots = 5;         // id / rating / bias slots (ids four chunks ahead)
+
+__device__ __forceinline__ int upk_off(int j, int KP) { return j * KP - ((j * (j - 1)) >> 1); }
+
+template <int NT>
+struct AlsWaveShape {
+    static constexpr int KP = 32 * NT;
+    static constexpr int NR = (KP + kWave - 1) / kWave;   // row-per-lane slots
+    static constexpr int CR = kAlsRingRows;
+    static constexpr int RPP = 8 / NT;                     // rows per 1-KiB DMA piece
+    static constexpr int LPR = 8 * NT;                     // lanes per row (16 B each)
+    static constexpr int PPC = CR / RPP;                   // pieces per chunk
+    static constexpr int elim_floats = 2 * KP + KP * (KP + 1) / 2;
+    static constexpr int gram_floats = kAlsRowBufs * CR * KP + 3 * kAlsIdSlots * kWave;
+    static constexpr int lds_floats = elim_floats > gram_floats ? elim_floats : gram_floats;
+    static constexpr int q(int I, int J) {                 // tile index of (I <= J)
+        int n = 0;
+        for (int JJ = 0; JJ < NT; ++JJ)
+            for (int II = 0; II <= JJ; ++II, ++n)
+                if (II == I && JJ == J) return n;
+        return -1;
+    }
+};
+
+__device__ __forceinline__ void als_lds_dma4(const void* src, void* lds_dst) {
+    __builtin_amdgcn_global_load_lds(
+        (__attribute__((address_space(1))) void*)const_cast<void*>(src),
+        (__attribute__((address_space(3))) void*)lds_dst, 4, 0, 0);
+}
+__device__ __forceinline__ void als_lds_dma16(const void* src, void* lds_dst) {
+    __builtin_amdgcn_global_load_lds(
+        (__attribute__((address_space(1))) void*)const_cast<void*>(src),
+        (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+// s_waitcnt vmcnt(n) for the few counts the Gramian pipeline needs
+template <int N1, int N2>
+__device__ __forceinline__ void als_wait_vm(int n) {
+    if (n == N1 + N2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N1 + N2) : "memory");
+    else if (n == N1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N1) : "memory");
+    else if (n == N2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N2) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int NT>
+__global__ __launch_bounds__(kWave) void k_als_wave(AlsArgs A) {
+    using TL = AlsTiles<NT>;
+    using SH = AlsWaveShape<NT>;
+    constexpr int KP = SH::KP, NR = SH::NR, NQ = TL::count;
+    constexpr int CR = SH::CR, RPP = SH::RPP, LPR = SH::LPR, PPC = SH::PPC;
+    extern __shared__ __align__(16) float lds[];
+
+    const int e = blockIdx.x;
+    const int64_t p0 = A.ptr[e], cnt = A.ptr[e + 1] - p0;
+    if (cnt == 0) return;                         // no ratings: parameters kept
+    als_stamp(A, 0);
+    const int L = threadIdx.x, c = L & 31, h = L >> 5;
+    const int k = A.k;
+
+    // ---- 1. Gramian ---------------------------------------------------------
+    constexpr int NB = kAlsRowBufs, NS = kAlsIdSlots;
+    float* Zb = lds;                              // [NB][CR][KP] row ring (DMA image)
+    int* ids = reinterpret_cast<int*>(lds + NB * CR * KP);   // [NS][64]
+    float* rts = lds + NB * CR * KP + NS * kWave;           // [NS][64] ratings
+    float* obs = rts + NS * kWave;                          // [NS][64] other-side biases
+    f32x16 m[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) m[q][i] = 0.f;
+    float fz[NT], sz[NT], ts = 0.f;
+#pragma unroll
+    for (int I = 0; I < NT; ++I) fz[I] = sz[I] = 0.f;
+    bool colok[NT];
+#pragma unroll
+    for (int I = 0; I < NT; ++I) colok[I] = 32 * I + c < k;
+    const int nch = (int)((cnt + CR - 1) / CR);
+    // stage A: ids and ratings of chunk X (lane L: row X CR + L, clamped to
+    // the entity's last rating so every id is a real one)
+    auto stage_a = [&](int X) __attribute__((always_inline)) {
+        const int64_t n = min((int64_t)X * CR + L, cnt - 1);
+        const int sl = X % NS;
+        als_lds_dma4(A.other + p0 + n, ids + sl * kWave);
+        als_lds_dma4(A.r + p0 + n, rts + sl * kWave);
+    };
+    // stage B: rows and other-side biases of chunk X (ids landed): piece p
+    // covers chunk rows p RPP .. p RPP + RPP-1, lane L 16 B of row p RPP +
+    // L / LPR (columns past k read the row start: masked where read)
+    auto stage_b = [&](int X) __attribute__((always_inline)) {
+        const int sl = X % NS;
+        float* dst = Zb + (X % NB) * CR * KP;
+        const int c4 = 4 * (L % LPR);
+#pragma unroll
+        for (int p = 0; p < PPC; ++p) {
+            const int idr = ids[sl * kWave + p * RPP + L / LPR];
+            als_lds_dma16(A.oq + (int64_t)idr * k + (c4 < k ? c4 : 0), dst + p * RPP * KP);
+        }
+        als_lds_dma4(A.ob + ids[sl * kWave + L], obs + sl * kWave);
+    };
+    // outstanding DMA after chunk cc's rows and chunk cc+2's ids: what the
+    // previous iteration issued, B(cc+1) then A(cc+3)
+    constexpr int NBQ = PPC + 1, NAQ = 2;
+    stage_a(0);
+    if (nch > 1) stage_a(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    stage_b(0);
+    if (nch > 2) stage_a(2);
+    if (nch > 1) stage_b(1);
+    if (nch > 3) stage_a(3);
+    for (int cc = 0; cc < nch; ++cc) {
+        als_wait_vm<NBQ, NAQ>((cc + 1 < nch ? NBQ : 0) + (cc + 3 < nch ? NAQ : 0));
+        __builtin_amdgcn_s_barrier();
+        if (cc + 2 < nch) stage_b(cc + 2);
+        if (cc + 4 < nch) stage_a(cc + 4);
+        const float* Zc = Zb + (cc % NB) * CR * KP;
+        const float* rc = rts + (cc % NS) * kWave;
+        const float* bc = obs + (cc % NS) * kWave;
+        const int64_t base = (int64_t)cc * CR;
+        // K-steps of this chunk (the last one stops at the entity's end);
+        // the LDS reads of step s + 1 are issued before the MFMAs of step s
+        const int steps = (int)min((int64_t)(CR / 2), (cnt - base + 1) >> 1);
+        float vn[NT], rn, bn;
+        auto ld = [&](int s_) __attribute__((always_inline)) {
+            const int n = 2 * s_ + h;
+#pragma unroll
+            for (int I = 0; I < NT; ++I) vn[I] = Zc[n * KP + 32 * I + c];
+            rn = rc[n];
+            bn = bc[n];
+        };
+        ld(0);
+#pragma unroll
+        for (int s = 0; s < CR / 2; ++s) {
+            if (s >= steps) break;
+            // the empty asm pins the values here (the loads stay unconditional
+            // and in flight across the previous step's MFMAs)
+#pragma unroll
+            for (int I = 0; I < NT; ++I) asm volatile("" : "+v"(vn[I]));
+            asm volatile("" : "+v"(rn), "+v"(bn));
+            const bool ok = base + 2 * s + h < cnt;
+            float zv[NT];
+#pragma unroll
+            for (int I = 0; I < NT; ++I) zv[I] = ok && colok[I] ? vn[I] : 0.f;
+            const float tv = ok ? (rn - A.mu) - bn : 0.f;
+            if (s + 1 < CR / 2) ld(s + 1);        // row s + 1 < CR: in the chunk
+            __builtin_amdgcn_sched_barrier(0);    // keep those reads ahead of the MFMAs
+#pragma unroll
+            for (int q = 0; q < NQ; ++q)
+                m[q] = __builtin_amdgcn_mfma_f32_32x32x2f32(zv[TL::I(q)], zv[TL::J(q)], m[q],
+                                                            0, 0, 0);
+#pragma unroll
+            for (int I = 0; I < NT; ++I) {
+                fz[I] = __builtin_fmaf(tv, zv[I], fz[I]);
+                sz[I] = sz[I] + zv[I];
+            }
+            ts += c == 0 ? tv : 0.f;
+        }
+    }
+    // column sums over both row halves; g = sum t over the rows (lanes c == 0)
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+        fz[I] = fz[I] + __shfl_xor(fz[I], 32, kWave);
+        sz[I] = sz[I] + __shfl_xor(sz[I], 32, kWave);
+    }
+    const float gsum = wave_sum(ts);
+    // right-hand columns row-per-lane: slot x holds row a = L + 64 x
+    float fr[NR], sr[NR];
+#pragma unroll
+    for (int x = 0; x < NR; ++x) {
+        const int a = L + 64 * x;
+        float fv = 0.f, sv = 0.f;
+#pragma unroll
+        for (int I = 2 * x; I < 2 * x + 2 && I < NT; ++I)
+            if ((I & 1) == h) { fv = fz[I]; sv = sz[I]; }
+        fr[x] = a < KP ? fv : 0.f;
+        sr[x] = a < KP ? sv : 0.f;
+    }
+    // + reg on the diagonal; padding dimensions (k <= a < KP) pivot 1
+#pragma unroll
+    for (int I = 0; I < NT; ++I) {
+        const int q = SH::q(I, I);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int ra = (i & 3) + 8 * (i >> 2) + 4 * h;
+            const float dg = 32 * I + c < k ? m[q][i] + A.reg : 1.f;
+            m[q][i] = ra == c ? dg : m[q][i];
+        }
+    }
+    __syncthreads();                              // the ring is reused below
+    als_stamp(A, 1);
+
+    // ---- 2. elimination -----------------------------------------------------
+    float* prow = lds;                            // [2][KP] published pivot rows
+    float* U = lds + 2 * KP;                      // packed rows of D U
+    // pivot state: u[J] = row j at column 32 J + c (both halves), r = 1 / d
+    float u[NT], r;
+    // extract row j (tile row Ij) into u / r and publish it to prow[j & 1], U
+    auto publish = [&](int Ij, int j) __attribute__((always_inline)) {
+        const int jl = j - 32 * Ij;
+        const int ij = (jl & 3) | ((jl >> 3) << 2);   // register of row j in its tile
+        const int hj = (jl >> 2) & 1;                 // lane half holding it
+        float* pr = prow + (j & 1) * KP;
+        const int uo = upk_off(j, KP) - j;
+        float dv = 0.f;
+#pragma unroll
+        for (int J = 0; J < NT; ++J) {
+            if (J < Ij) continue;
+            const float v = m[SH::q(Ij, J)][ij];
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v),
+                                                             false, false);
+            const float uv = __uint_as_float(hj ? sw[1] : sw[0]);
+            const int b = 32 * J + c;
+            u[J] = b > j ? uv : 0.f;
+            if (h == 0) {
+                pr[b] = u[J];
+                if (b >= j) U[uo + b] = uv;
+            }
+            if (J == Ij) dv = uv;
+        }
+        const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), jl));
+        // 1/d: v_rcp_f32 (1 ulp) and one Newton step
+        float rr = __builtin_amdgcn_rcpf(d);
+        r = rr * __builtin_fmaf(-d, rr, 2.f);
+    };
+    // rank-1 update of tile row I by pivot j (published in prow[j & 1])
+    auto update_row = [&](int I, const float* pr, const float (&w)[NT]) __attribute__((always_inline)) {
+        float l[16];
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+            const float4 v4 = *reinterpret_cast<const float4*>(pr + 32 * I + 8 * qq + 4 * h);
+            l[4 * qq + 0] = v4.x; l[4 * qq + 1] = v4.y;
+            l[4 * qq + 2] = v4.z; l[4 * qq + 3] = v4.w;
+        }
+#pragma unroll
+        for (int J = 0; J < NT; ++J) {
+            if (J < I) continue;
+            const int q = SH::q(I, J);
+            const f32x2 wv = {w[J], w[J]};
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {     // v_pk_fma_f32: two rows per instruction
+                f32x2 mv = {m[q][i], m[q][i + 1]};
+                const f32x2 lv = {l[i], l[i + 1]};
+                mv = __builtin_elementwise_fma(lv, wv, mv);
+                m[q][i] = mv[0];
+                m[q][i + 1] = mv[1];
+            }
+        }
+    };
+#pragma unroll
+    for (int Ij = 0; Ij < NT; ++Ij) {
+        publish(Ij, 32 * Ij);
+#pragma clang loop unroll(disable)
+        for (int jl = 0; jl < 32; ++jl) {
+            const int j = 32 * Ij + jl;
+            const float* pr = prow + (j & 1) * KP;
+            float w[NT];                          // -(row j at this lane's columns) / d
+#pragma unroll
+            for (int J = 0; J < NT; ++J) w[J] = J < Ij ? 0.f : u[J] * -r;
+            const float fjr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fr[Ij >> 1]), j & 63)) * -r;
+            const float sjr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sr[Ij >> 1]), j & 63)) * -r;
+            // the published row is read from LDS, never forwarded from this
+            // lane's own stores: one wave, so the barrier is the lgkmcnt drain
+            __syncthreads();
+            update_row(Ij, pr, w);
+            if (jl < 31) publish(Ij, j + 1);      // overlaps the updates below
+#pragma unroll
+            for (int I = Ij + 1; I < NT; ++I) update_row(I, pr, w);
+#pragma unroll
+            for (int x = 0; x < NR; ++x) {
+                // rows up to j keep their value (the published row only
+                // covers tile columns >= Ij; earlier columns are stale)
+                const int a = L + 64 * x;
+                const float la = a > j && a < KP ? pr[a] : 0.f;
+                fr[x] = __builtin_fmaf(la, fjr, fr[x]);
+                sr[x] = __builtin_fmaf(la, sjr, sr[x]);
+            }
+        }
+    }
+    als_stamp(A, 2);
+
+    // ---- 3. border (Schur complement) and back substitution -------------------
+    __syncthreads();
+    float dinv[NR], wv[NR], acc[NR], xs[NR];
+    float num = 0.f, den = 0.f;
+#pragma unroll
+    for (int x = 0; x < NR; ++x) {
+        const int a = L + 64 * x;
+        const float dd = a < KP ? U[upk_off(a, KP)] : 1.f;
+        dinv[x] = 1.f / dd;
+        num += (sr[x] * fr[x]) * dinv[x];
+        den += (sr[x] * sr[x]) * dinv[x];
+    }
+    num = wave_sum(num);
+    den = wave_sum(den);
+    const float bias = (gsum - num) / (((float)cnt + A.reg) - den);
+#pragma unroll
+    for (int x = 0; x < NR; ++x) {
+        wv[x] = (fr[x] - bias * sr[x]) * dinv[x];
+        acc[x] = 0.f;
+        xs[x] = 0.f;
+    }
+    // x_t = w_t - acc_t, t = KP-1 .. 0; acc_a += (U[a][t] / D_a) x_t for a < t
+#pragma unroll
+    for (int xt = NR - 1; xt >= 0; --xt) {
+#pragma clang loop unroll_count(4)
+        for (int tl = (xt == NR - 1 ? KP - 64 * xt : 64) - 1; tl >= 0; --tl) {
+            const int t = 64 * xt + tl;
+            float ua[NR];
+#pragma unroll
+            for (int x = 0; x < NR; ++x) {
+                const int a = L + 64 * x;
+                ua[x] = (x <= xt && a < t) ? U[upk_off(a, KP) + t - a] : 0.f;
+            }
+            const float cand = wv[xt] - acc[xt];
+            const float xv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand), tl));
+            if (L == tl) xs[xt] = xv;
+#pragma unroll
+            for (int x = 0; x <= xt; ++x) acc[x] = acc[x] + (ua[x] * dinv[x]) * xv;
+        }
+    }
+    float* out = A.feat + (int64_t)e * k;
+#pragma unroll
+    for (int x = 0; x < NR; ++x) {
+        const int a = L + 64 * x;
+        if (a < k) out[a] = xs[x];
+    }
+    if (L == 0) A.bias[e] = bias;
+    als_stamp(A, 3);
+}
+
+template <int NT>
+int als_go_wave(const AlsArgs& a, int32_t n, hipStream_t stream) {
+    const size_t lds = (size_t)AlsWaveShape<NT>::lds_floats * sizeof(float);
+    auto kfn = k_als_wave<NT>;
+    MF_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(kfn),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    hipLaunchKernelGGL(kfn, dim3((unsigned)n), dim3(kWave), lds, stream, a);
+    MF_HIP_CHECK(hipGetLastError());
+    return MF_OK;
+}
+
 template <int NT>
 int als_go(const AlsArgs& a, int32_t n, hipStream_t stream) {
     constexpr int KP = NT * 32;
@@ -474,9 +850,22 @@ static int als_sweep(const int64_t* entity_ptr, const int32_t* other_ids,
     a.bias = static_cast<float*>(biases); a.feat = static_cast<float*>(features);
     a.k = n_factors; a.mu = (float)global_mean; a.reg = (float)reg; a.probe = probe;
     hipStream_t s = (hipStream_t)stream;
-    if (n_factors <= 32) return als_go<1>(a, n_entities, s);
-    if (n_factors <= 64) return als_go<2>(a, n_entities, s);
-    return als_go<4>(a, n_entities, s);           // 96 columns do not tile 256 lanes
+    // k_als_wave (default); MF_ALS_KERNEL=block selects the 4-wave
+    // k_als_solve (A/B probes)
+    const char* ev = std::getenv("MF_ALS_KERNEL");
+    if (ev && std::strcmp(ev, "block") == 0) {
+        if (n_factors <= 32) return als_go<1>(a, n_entities, s);
+        if (n_factors <= 64) return als_go<2>(a, n_entities, s);
+        return als_go<4>(a, n_entities, s);       // 96 columns do not tile 256 lanes
+    }
+    if (n_factors % 4 != 0) {                     // rows not 16-byte aligned for the DMA
+        if (n_factors <= 32) return als_go<1>(a, n_entities, s);
+        if (n_factors <= 64) return als_go<2>(a, n_entities, s);
+        return als_go<4>(a, n_entities, s);
+    }
+    if (n_factors <= 32) return als_go_wave<1>(a, n_entities, s);
+    if (n_factors <= 64) return als_go_wave<2>(a, n_entities, s);
+    return als_go_wave<4>(a, n_entities, s);
 }
 
 extern "C" int mf_als_sweep(const int64_t* entity_ptr, const int32_t* other_ids,
