@@ -463,8 +463,8 @@ __global__ __launch_bounds__(kAlsThreads, 2) void k_als_solve(AlsArgs A) {
 // Ranks with n_factors % 4 != 0 (rows not 16-byte aligned for the DMA) use
 // k_als_solve.
 constexpr int kAlsRingRows = 16;       // rows per ring chunk (8 K-steps)
-constexpr int kAlsRowBufs = 3;         // ring chunks (rows two chunks ahead)
-constexpr int kAlsIdSlots = 5;         // id / rating / bias slots (ids four chunks ahead)
+constexpr int kAlsRowBufs = 2;         // ring chunks (rows one chunk ahead)
+constexpr int kAlsIdSlots = 4;         // id / rating / bias slots (ids three chunks ahead)
 
 __device__ __forceinline__ int upk_off(int j, int KP) { return j * KP - ((j * (j - 1)) >> 1); }
 
@@ -476,7 +476,7 @@ struct AlsWaveShape {
     static constexpr int RPP = 8 / NT;                     // rows per 1-KiB DMA piece
     static constexpr int LPR = 8 * NT;                     // lanes per row (16 B each)
     static constexpr int PPC = CR / RPP;                   // pieces per chunk
-    static constexpr int elim_floats = 2 * KP + KP * (KP + 1) / 2;
+    static constexpr int elim_floats = 2 * KP + 32 * 33;   // pivot rows + transpose scratch
     static constexpr int gram_floats = kAlsRowBufs * CR * KP + 3 * kAlsIdSlots * kWave;
     static constexpr int lds_floats = elim_floats > gram_floats ? elim_floats : gram_floats;
     static constexpr int q(int I, int J) {                 // tile index of (I <= J)
@@ -499,17 +499,8 @@ __device__ __forceinline__ void als_lds_dma16(const void* src, void* lds_dst) {
         (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
 }
 
-// s_waitcnt vmcnt(n) for the few counts the Gramian pipeline needs
-template <int N1, int N2>
-__device__ __forceinline__ void als_wait_vm(int n) {
-    if (n == N1 + N2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N1 + N2) : "memory");
-    else if (n == N1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N1) : "memory");
-    else if (n == N2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N2) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 template <int NT>
-__global__ __launch_bounds__(kWave) void k_als_wave(AlsArgs A) {
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(2))) void k_als_wave(AlsArgs A) {
     using TL = AlsTiles<NT>;
     using SH = AlsWaveShape<NT>;
     constexpr int KP = SH::KP, NR = SH::NR, NQ = TL::count;
@@ -563,22 +554,21 @@ __global__ __launch_bounds__(kWave) void k_als_wave(AlsArgs A) {
         }
         als_lds_dma4(A.ob + ids[sl * kWave + L], obs + sl * kWave);
     };
-    // outstanding DMA after chunk cc's rows and chunk cc+2's ids: what the
-    // previous iteration issued, B(cc+1) then A(cc+3)
-    constexpr int NBQ = PPC + 1, NAQ = 2;
+    // iteration cc issues B(cc+1) then A(cc+3); at its start chunk cc's rows
+    // (B, previous iteration) and chunk cc+1's ids (A, two back) must have
+    // landed, so only A(cc+2), issued after B(cc), may still be in flight
     stage_a(0);
     if (nch > 1) stage_a(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     stage_b(0);
     if (nch > 2) stage_a(2);
-    if (nch > 1) stage_b(1);
-    if (nch > 3) stage_a(3);
     for (int cc = 0; cc < nch; ++cc) {
-        als_wait_vm<NBQ, NAQ>((cc + 1 < nch ? NBQ : 0) + (cc + 3 < nch ? NAQ : 0));
+        if (cc + 2 < nch) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
-        if (cc + 2 < nch) stage_b(cc + 2);
-        if (cc + 4 < nch) stage_a(cc + 4);
+        if (cc + 1 < nch) stage_b(cc + 1);
+        if (cc + 3 < nch) stage_a(cc + 3);
         const float* Zc = Zb + (cc % NB) * CR * KP;
         const float* rc = rts + (cc % NS) * kWave;
         const float* bc = obs + (cc % NS) * kWave;
@@ -657,16 +647,17 @@ __global__ __launch_bounds__(kWave) void k_als_wave(AlsArgs A) {
 
     // ---- 2. elimination -----------------------------------------------------
     float* prow = lds;                            // [2][KP] published pivot rows
-    float* U = lds + 2 * KP;                      // packed rows of D U
-    // pivot state: u[J] = row j at column 32 J + c (both halves), r = 1 / d
-    float u[NT], r;
-    // extract row j (tile row Ij) into u / r and publish it to prow[j & 1], U
+    // pivot state: u[J] = row j at column 32 J + c (both halves), d, r = 1 / d
+    float u[NT], r, dpiv;
+    float dreg[NR];                               // D_a, row-per-lane (rows L + 64 x)
+#pragma unroll
+    for (int x = 0; x < NR; ++x) dreg[x] = 1.f;
+    // extract row j (tile row Ij) into u / d / r and publish it to prow[j & 1]
     auto publish = [&](int Ij, int j) __attribute__((always_inline)) {
         const int jl = j - 32 * Ij;
         const int ij = (jl & 3) | ((jl >> 3) << 2);   // register of row j in its tile
         const int hj = (jl >> 2) & 1;                 // lane half holding it
         float* pr = prow + (j & 1) * KP;
-        const int uo = upk_off(j, KP) - j;
         float dv = 0.f;
 #pragma unroll
         for (int J = 0; J < NT; ++J) {
@@ -677,16 +668,13 @@ __global__ __launch_bounds__(kWave) void k_als_wave(AlsArgs A) {
             const float uv = __uint_as_float(hj ? sw[1] : sw[0]);
             const int b = 32 * J + c;
             u[J] = b > j ? uv : 0.f;
-            if (h == 0) {
-                pr[b] = u[J];
-                if (b >= j) U[uo + b] = uv;
-            }
+            pr[b] = u[J];                         // both halves: same address, same value
             if (J == Ij) dv = uv;
         }
-        const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), jl));
+        dpiv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dv), jl));
         // 1/d: v_rcp_f32 (1 ulp) and one Newton step
-        float rr = __builtin_amdgcn_rcpf(d);
-        r = rr * __builtin_fmaf(-d, rr, 2.f);
+        float rr = __builtin_amdgcn_rcpf(dpiv);
+        r = rr * __builtin_fmaf(-dpiv, rr, 2.f);
     };
     // rank-1 update of tile row I by pivot j (published in prow[j & 1])
     auto update_row = [&](int I, const float* pr, const float (&w)[NT]) __attribute__((always_inline)) {
@@ -724,6 +712,7 @@ __global__ __launch_bounds__(kWave) void k_als_wave(AlsArgs A) {
             for (int J = 0; J < NT; ++J) w[J] = J < Ij ? 0.f : u[J] * -r;
             const float fjr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fr[Ij >> 1]), j & 63)) * -r;
             const float sjr = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sr[Ij >> 1]), j & 63)) * -r;
+            dreg[Ij >> 1] = L == (j & 63) ? dpiv : dreg[Ij >> 1];
             // the published row is read from LDS, never forwarded from this
             // lane's own stores: one wave, so the barrier is the lgkmcnt drain
             __syncthreads();
@@ -745,14 +734,18 @@ __global__ __launch_bounds__(kWave) void k_als_wave(AlsArgs A) {
     als_stamp(A, 2);
 
     // ---- 3. border (Schur complement) and back substitution -------------------
-    __syncthreads();
-    float dinv[NR], wv[NR], acc[NR], xs[NR];
+    // The eliminated rows D U stay in the tile registers (row j is never
+    // updated after its pivot).  Bottom-up per tile row I: (i) the solved
+    // tiles J > I contribute U_IJ x_J, lane partials reduced through LDS;
+    // (ii) the diagonal tile, transposed through LDS, is solved in 32
+    // sequential column steps: lane (c, h) keeps row 32 I + c's partial sum
+    // over the columns its half holds, x_t = (r_t - both halves' sums) / D_t.
+    float* S = lds + 2 * KP;                      // [32][33] transpose scratch
+    float dinv[NR], y[NR];
     float num = 0.f, den = 0.f;
 #pragma unroll
     for (int x = 0; x < NR; ++x) {
-        const int a = L + 64 * x;
-        const float dd = a < KP ? U[upk_off(a, KP)] : 1.f;
-        dinv[x] = 1.f / dd;
+        dinv[x] = 1.f / dreg[x];
         num += (sr[x] * fr[x]) * dinv[x];
         den += (sr[x] * sr[x]) * dinv[x];
     }
@@ -760,35 +753,54 @@ __global__ __launch_bounds__(kWave) void k_als_wave(AlsArgs A) {
     den = wave_sum(den);
     const float bias = (gsum - num) / (((float)cnt + A.reg) - den);
 #pragma unroll
-    for (int x = 0; x < NR; ++x) {
-        wv[x] = (fr[x] - bias * sr[x]) * dinv[x];
-        acc[x] = 0.f;
-        xs[x] = 0.f;
-    }
-    // x_t = w_t - acc_t, t = KP-1 .. 0; acc_a += (U[a][t] / D_a) x_t for a < t
+    for (int x = 0; x < NR; ++x) y[x] = fr[x] - bias * sr[x];
+    float xc[NT];                                 // x_{32 J + c} at lane c (both halves)
 #pragma unroll
-    for (int xt = NR - 1; xt >= 0; --xt) {
-#pragma clang loop unroll_count(4)
-        for (int tl = (xt == NR - 1 ? KP - 64 * xt : 64) - 1; tl >= 0; --tl) {
-            const int t = 64 * xt + tl;
-            float ua[NR];
+    for (int J = 0; J < NT; ++J) xc[J] = 0.f;
 #pragma unroll
-            for (int x = 0; x < NR; ++x) {
-                const int a = L + 64 * x;
-                ua[x] = (x <= xt && a < t) ? U[upk_off(a, KP) + t - a] : 0.f;
+    for (int I = NT - 1; I >= 0; --I) {
+        const int src = 32 * (I & 1) + c;         // row 32 I + c in the row-per-lane slots
+        const float yc = __shfl(y[I >> 1], src, kWave);
+        const float dc = __shfl(dinv[I >> 1], src, kWave);
+        float off = 0.f;
+        if (I < NT - 1) {
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float pv = 0.f;
+#pragma unroll
+                for (int J = I + 1; J < NT; ++J) pv = __builtin_fmaf(m[SH::q(I, J)][i], xc[J], pv);
+                S[((i & 3) + 8 * (i >> 2) + 4 * h) * 33 + c] = pv;
             }
-            const float cand = wv[xt] - acc[xt];
-            const float xv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand), tl));
-            if (L == tl) xs[xt] = xv;
+            __syncthreads();
+            float sacc = 0.f;
 #pragma unroll
-            for (int x = 0; x <= xt; ++x) acc[x] = acc[x] + (ua[x] * dinv[x]) * xv;
+            for (int cc2 = 0; cc2 < 16; ++cc2) sacc += S[c * 33 + 16 * h + cc2];
+            off = sacc + __shfl_xor(sacc, 32, kWave);
         }
-    }
-    float* out = A.feat + (int64_t)e * k;
+        const float rc = yc - off;
+        __syncthreads();
 #pragma unroll
-    for (int x = 0; x < NR; ++x) {
-        const int a = L + 64 * x;
-        if (a < k) out[a] = xs[x];
+        for (int i = 0; i < 16; ++i) S[((i & 3) + 8 * (i >> 2) + 4 * h) * 33 + c] = m[SH::q(I, I)][i];
+        __syncthreads();
+        float T[16];                              // T[i] = U[32 I + c][32 I + ra(i, h)]
+#pragma unroll
+        for (int i = 0; i < 16; ++i) T[i] = S[c * 33 + (i & 3) + 8 * (i >> 2) + 4 * h];
+        float acc = 0.f, xi = 0.f;
+#pragma unroll
+        for (int tl = 31; tl >= 0; --tl) {
+            const int it = (tl & 3) + 4 * (tl >> 3), ht = (tl >> 2) & 1;
+            const float s0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rc - acc), tl));
+            const float s1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(acc), 32 + tl));
+            const float dt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(dc), tl));
+            const float xv = (s0 - s1) * dt;
+            xi = c == tl ? xv : xi;
+            const float uct = (h == ht && c < tl) ? T[it] : 0.f;
+            acc = __builtin_fmaf(uct, xv, acc);
+        }
+        xc[I] = xi;
+        float* out = A.feat + (int64_t)e * k;
+        if (h == 0 && 32 * I + c < k) out[32 * I + c] = xi;
     }
     if (L == 0) A.bias[e] = bias;
     als_stamp(A, 3);
