@@ -474,14 +474,18 @@ def main() -> int:
                     help="do not bracket the SGD / RMSE phases with hipEvents")
     ap.add_argument("--blocks", type=int, default=None,
                     help="strata: B (probes; default: engine.choose_strata_blocks)")
-    ap.add_argument("--waves", type=int, default=None, choices=[8, 16],
-                    help="strata: waves per workgroup (default: by the plan's slot fill)")
+    ap.add_argument("--waves", type=int, default=None, choices=[4, 8, 16],
+                    help="strata: waves per workgroup (default: by the plan's slot fill; "
+                         "4 = the 8-wave plan on the narrow 4-wave kernels)")
     ap.add_argument("--schedule", default="strata", choices=["strata", "colored"],
                     help="strata: B x B blocks, item slabs in LDS (mf_strata.hpp); "
                          "colored: one launch per edge colour (mf_rows.hpp)")
     ap.add_argument("--delta-scale", type=float, default=None,
                     help="N > 1: weight of the all-reduced item deltas (default 1/N, "
                          "model averaging; 1.0 = plain gradient sum)")
+    ap.add_argument("--rmse-overlap", action="store_true",
+                    help="one GPU: run each epoch's RMSE pass on a side stream from a "
+                         "parameter snapshot, beside the next epoch's sweep")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 process group: nccl (= RCCL, one GPU per rank) or gloo "
                          "(rehearsal: ranks may share a GPU, LOCAL_RANK mod device count)")
@@ -549,8 +553,10 @@ def main() -> int:
         strat_sizes = plan.stratum_sizes()           # ratings per stratum (launch)
         fill = n_local / max(plan.n_positions, 1)
         sched_desc = (f"strata (B={nb}: {nb} launches/epoch, item slabs in LDS, "
-                      f"{plan.NS} user-owned slots ({plan.NS * 1024 // strata_slots(k, eng.dcode)} "
-                      f"threads/workgroup) x {int(plan.n_steps.max())} steps max "
+                      f"{plan.NS} user-owned slots "
+                      f"({256 if plan.narrow else plan.NS * 1024 // strata_slots(k, eng.dcode)} "
+                      f"threads/workgroup{', narrow lane groups' if plan.narrow else ''}) x "
+                      f"{int(plan.n_steps.max())} steps max "
                       f"per block, {fill:.1%} slot fill)")
     else:
         nb = eng.prepare_colored()
@@ -615,6 +621,13 @@ def main() -> int:
     launches_per_epoch = nb if strata else int(np.sum(np.diff(eng.colored) > 0))
     persistent = False
     events = []     # (sgd start, sgd end, exchange end, sse end) per timed epoch
+    # --rmse-overlap (one GPU): the RMSE pass of epoch e runs on a side stream
+    # from a snapshot of the parameters, beside the SGD sweep of epoch e + 1.
+    # Off by default: at C3 the persistent sweep cannot start its workgroups
+    # while the RMSE kernel holds the CUs, so the two serialise and the
+    # snapshot copy is pure cost (11.83 vs 11.67 ms per epoch; C2 1.125 vs
+    # 1.146 ms) -- DESIGN.md section 5
+    overlap = world == 1 and args.rmse_overlap
 
     def epoch(ep, timed):
         # hipEvents on the stream the kernels run on (torch's current stream,
@@ -631,7 +644,10 @@ def main() -> int:
         end()
         if ev:
             ev[2].record()
-        eng.sse_async(ep)
+        if overlap:
+            eng.sse_overlap(ep, timing=bool(ev))
+        else:
+            eng.sse_async(ep)
         if ev:
             ev[3].record()
             events.append(ev)
@@ -723,6 +739,13 @@ def main() -> int:
             phases = {"sgd_ms_per_epoch": sgd_s / len(events) * 1e3,
                       "rmse_ms_per_epoch": sse_s / len(events) * 1e3,
                       "sgd_updates_per_s": n_local * len(events) / sgd_s}
+            if overlap:
+                side = (eng._ov or {}).get("events", [])
+                phases["rmse_ms_per_epoch"] = (sum(a.elapsed_time(b) for a, b in side)
+                                               / max(len(side), 1))
+                phases["snapshot_ms_per_epoch"] = sse_s / len(events) * 1e3
+                phases["rmse_overlapped"] = ("on a side stream, from a device snapshot of "
+                                             "the parameters, beside the next epoch's sweep")
             if world > 1:
                 phases["exchange_ms_per_epoch"] = exch_s / len(events) * 1e3
         out = {
@@ -737,7 +760,9 @@ def main() -> int:
                        "schedule": sched_desc,
                        "parallelism": f"user-sharded dp{world}" if world > 1 else "single GPU",
                        "item_delta_scale": None if exch is None else exch.scale,
-                       "step": "one epoch: SGD sweep + training-RMSE pass"},
+                       "step": "one epoch: SGD sweep + training-RMSE pass" +
+                               (" (epoch e's RMSE overlapped with epoch e+1's sweep)"
+                                if overlap else "")},
             "final_rmse": rmse[-1], "rmse_per_epoch": rmse,
             "roofline": roofline, "phases": phases,
             "cpu_baseline": cpu_baseline, "parity": parity,

@@ -62,9 +62,13 @@ enum {
                                  stratum when the grid cannot be co-resident) */
     MF_FLAG_DEEP_PIPE = 32,   /* with MF_FLAG_PERSISTENT: user rows gathered two
                                  steps ahead (blocks of few steps)               */
-    MF_FLAG_NO_COOP = 64      /* with MF_FLAG_PERSISTENT: plain launch instead of
+    MF_FLAG_NO_COOP = 64,     /* with MF_FLAG_PERSISTENT: plain launch instead of
                                  hipLaunchCooperativeKernel (diagnostic A/B; the
                                  occupancy check is then the only guard)         */
+    MF_FLAG_NARROW = 128      /* strata: a plan built for mf_strata_slots_waves(k,
+                                 dtype, 4) runs on 4-wave workgroups whose lane
+                                 groups are half as wide (two vectors per lane;
+                                 FP32, n_factors a multiple of 4 up to 32) */
 };
 
 const char* mf_last_error(void);
@@ -211,7 +215,9 @@ int32_t mf_strata_slots(int32_t n_factors, int32_t dtype);
 /* The same for a workgroup of `waves` waves: 16 (the default) or, FP32 with
  * n_factors <= 64 only, 8 -- a plan built with that many slots runs the
  * 8-wave kernels (blocks whose step count is set by the item degree, not by
- * the slot count); -1 where the layout has no 8-wave kernels. */
+ * the slot count); 4 = the narrow form of the 8-wave plan (same slot count,
+ * run with MF_FLAG_NARROW; FP32, n_factors a multiple of 4 up to 32); -1
+ * where the layout has no such kernels. */
 int32_t mf_strata_slots_waves(int32_t n_factors, int32_t dtype, int32_t waves);
 
 /*

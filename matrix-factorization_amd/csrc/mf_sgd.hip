@@ -285,7 +285,7 @@ extern "C" int mf_strata_status(const void* workspace, int32_t n_blocks, void* s
 
 extern "C" int32_t mf_strata_slots_waves(int32_t n_factors, int32_t dtype, int32_t waves) {
     if (n_factors < 0 || n_factors > kMaxFactors || (dtype != MF_F32 && dtype != MF_F64) ||
-        (waves != 16 && waves != 8)) {
+        (waves != 16 && waves != 8 && waves != 4)) {
         set_error("mf_strata_slots_waves: n_factors=%d / dtype=%d / waves=%d invalid", n_factors,
                   dtype, waves);
         return -1;

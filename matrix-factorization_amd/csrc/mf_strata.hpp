@@ -649,6 +649,18 @@ constexpr bool strata_has_8_waves() {
     return std::is_same<T, float>::value && V == 1;
 }
 
+// the narrow form (MF_FLAG_NARROW): 4 waves whose lane groups are half as
+// wide, two vectors per lane -- the 8-wave kernel's slot count on half the
+// waves, i.e. fewer instructions per slot and step (the dot product's group
+// sum one DPP level shorter, the sigmoid / bias / address work per slot
+// spread over half the lanes).  FP32 rows of one vector per lane whose slot
+// count matches (k <= 32 here).
+template <typename T, int W, int GS, int V>
+constexpr bool strata_has_narrow() {
+    if constexpr (!strata_has_8_waves<T, V>() || GS < 2) return false;
+    else return strata_slots<T, W, GS / 2, 2 * V, 4>() == strata_slots<T, W, GS, V, 8>();
+}
+
 template <typename T>
 struct StrataSlots {
     int waves;
@@ -657,6 +669,8 @@ struct StrataSlots {
         if (waves == 16) return strata_slots<T, W, GS, V, 16>();
         if constexpr (strata_has_8_waves<T, V>())
             if (waves == 8) return strata_slots<T, W, GS, V, 8>();
+        if constexpr (strata_has_narrow<T, W, GS, V>())
+            if (waves == 4) return strata_slots<T, W, GS / 2, 2 * V, 4>();
         return -1;
     }
 };
@@ -670,7 +684,15 @@ struct StrataRun {
         constexpr int S = strata_group_slots<T, W, GS, V>();
         if (p.n_slots == strata_slots<T, W, GS, V, 16>()) return go<W, GS, V, KERN, S, 16>();
         if constexpr (strata_has_8_waves<T, V>()) {
-            if (p.n_slots == strata_slots<T, W, GS, V, 8>()) return go<W, GS, V, KERN, S, 8>();
+            if (p.n_slots == strata_slots<T, W, GS, V, 8>()) {
+                if constexpr (strata_has_narrow<T, W, GS, V>()) {
+                    if (p.flags & MF_FLAG_NARROW) {
+                        constexpr int GS2 = GS / 2, V2 = 2 * V;
+                        return go<W, GS2, V2, KERN, strata_group_slots<T, W, GS2, V2>(), 4>();
+                    }
+                }
+                return go<W, GS, V, KERN, S, 8>();
+            }
         }
         set_error("plan has %d slots per step, the n_factors=%d layout needs %d (16 waves)%s",
                   p.n_slots, p.k, strata_slots<T, W, GS, V, 16>(),

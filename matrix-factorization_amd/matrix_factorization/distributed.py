@@ -222,6 +222,7 @@ def sharded_epochs(engine: SGDEngine, exchange: Optional[ReplicaExchange], n_epo
 
 def global_rmse(engine: SGDEngine, n_epochs: int, n_total: int, group=None) -> list:
     """Per-epoch training RMSE over all ranks (one all-reduce for all epochs)."""
+    engine.sse_join()                     # an overlapped SSE (sse_overlap) has landed
     sse = engine.sse_buf[:n_epochs].clone()
     if dist.is_available() and dist.is_initialized():
         dist.all_reduce(sse, op=dist.ReduceOp.SUM, group=group)

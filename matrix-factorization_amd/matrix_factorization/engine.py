@@ -161,6 +161,8 @@ class StrataPlan:
     ``n_steps`` x ``NS`` rating slots (``sched``: rating index per position,
     -1 = idle slot)."""
 
+    narrow = False      # built for the narrow 4-wave kernels (MF_FLAG_NARROW)
+
     def __init__(self, B, NS, ubnd, ibnd, bstep, sched):
         self.B, self.NS = int(B), int(NS)
         self.ubnd, self.ibnd, self.bstep, self.sched = ubnd, ibnd, bstep, sched
@@ -337,6 +339,7 @@ class SGDEngine:
         self.ws = torch.empty((ws + 7) // 8, dtype=torch.float64, device=self.dev)
         self.sse_buf = torch.zeros(16, dtype=torch.float64, device=self.dev)
         self.P = self.Q = self.bu = self.bi = None
+        self._ov = None              # sse_overlap state (side stream, snapshot)
 
     # ---------------------------------------------------------- plumbing
     @property
@@ -418,7 +421,8 @@ class SGDEngine:
         host arrays keep the original rating order.
 
         ``waves``: workgroup size of the strata kernels, 16 or 8 (FP32,
-        k <= 64).  None = by the plan: when the 16-wave plan fills fewer
+        k <= 64), or 4: the 8-wave plan run by the narrow 4-wave kernels
+        (MF_FLAG_NARROW; FP32, k a multiple of 4 up to 32).  None = by the plan: when the 16-wave plan fills fewer
         than 70 % of its slots (steps bound by the item degree of the
         blocks, not by the slot count), the 8-wave plan is built too and
         kept if steps * waves -- the per-CU VALU issue of an epoch, which
@@ -433,7 +437,7 @@ class SGDEngine:
             ub = balanced_bounds(self.u_host, self.n_users, B)
             ib = balanced_bounds(self.i_host, self.n_items, B)
         env = os.environ.get("MF_STRATA_WAVES")
-        if waves is None and env in ("8", "16"):
+        if waves is None and env in ("4", "8", "16"):
             waves = int(env)
         cand = [waves] if waves is not None else [16, 8]
         best = None
@@ -453,6 +457,7 @@ class SGDEngine:
                 break                       # well filled: the 16-wave plan it is
         _, ns, sched, bstep = best
         plan = StrataPlan(B, ns, ub, ib, bstep, sched)
+        plan.narrow = waves == 4
         plan.to_device(self.u, self.i, self.r, self.dev)
         self.strata = plan
         return plan
@@ -492,6 +497,8 @@ class SGDEngine:
             flags |= _lib.MF_FLAG_DEEP_PIPE
         if os.environ.get("MF_STRATA_COOP") == "0" or _under_rocprofiler():
             flags |= _lib.MF_FLAG_NO_COOP
+        if pl.narrow:
+            flags |= _lib.MF_FLAG_NARROW
         wsb = int(_lib.load().mf_strata_workspace_bytes(pl.B, len(seq)))
         old = getattr(self, "_strata_ws", None)
         if old is None or old.numel() * 4 < wsb:
@@ -644,7 +651,61 @@ class SGDEngine:
                           0 if offs is None else len(offs) - 1, _tp(self.ws), out,
                           self.stream)
 
+    def sse_overlap(self, slot: int, timing: bool = False) -> None:
+        """The training SSE of the current parameters into slot ``slot``,
+        computed off the critical path: the parameters are copied to a device
+        snapshot on the main stream (what the next epoch's sweep then
+        overwrites), and mf_sse reads the snapshot on a side stream, so the
+        next epoch's SGD runs while it does.  Same value as sse_async (the
+        same kernel on the same parameter values); sse_values() waits for
+        the side stream."""
+        if self.bias_only or self.n == 0:
+            self.sse_async(slot)
+            return
+        main = torch.cuda.current_stream(self.dev)
+        ov = self._ov
+        if ov is None:
+            ov = self._ov = dict(side=torch.cuda.Stream(self.dev), done=None,
+                                 P=torch.empty_like(self.P), Q=torch.empty_like(self.Q),
+                                 bu=torch.empty_like(self.bu), bi=torch.empty_like(self.bi),
+                                 ws=torch.empty_like(self.ws))
+        if self.sse_buf.numel() < slot + 1:
+            ov["side"].synchronize()             # no SSE writes into the old buffer
+            self._ensure_sse_slots(slot + 1)
+        if ov["done"] is not None:
+            main.wait_event(ov["done"])          # the previous SSE has read the snapshot
+        for name in ("P", "Q", "bu", "bi"):
+            ov[name].copy_(getattr(self, name))
+        ready = torch.cuda.Event()
+        ready.record(main)
+        side = ov["side"]
+        side.wait_event(ready)
+        if timing:                                 # (start, end) on the side stream
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record(side)
+            ov.setdefault("events", []).append(ev)
+        out = _VOID(self.sse_buf.data_ptr() + 8 * slot)
+        offs = self.eval_offs
+        with torch.cuda.device(self.dev):
+            _lib.call("mf_sse", _tp(self.eu), _tp(self.ei), _tp(self.er), self.n,
+                      self.global_mean, _tp(ov["bu"]), _tp(ov["bi"]), _tp(ov["P"]),
+                      _tp(ov["Q"]), self.n_users, self.n_items, self.k, self.kcode,
+                      self.dcode, self.gamma, self.min_rating, self.max_rating, _np(offs),
+                      0 if offs is None else len(offs) - 1, _tp(ov["ws"]), out,
+                      _VOID(side.cuda_stream))
+        if timing:
+            ov["events"][-1][1].record(side)
+        done = torch.cuda.Event()
+        done.record(side)
+        ov["done"] = done
+
+    def sse_join(self) -> None:
+        """Make the main stream wait for an overlapped SSE (sse_overlap)."""
+        if self._ov is not None and self._ov["done"] is not None:
+            torch.cuda.current_stream(self.dev).wait_event(self._ov["done"])
+
     def sse_values(self, n_slots: int) -> np.ndarray:
+        self.sse_join()
         return self.sse_buf[:n_slots].cpu().numpy().copy()
 
     def rmse_values(self, n_slots: int) -> list:

@@ -114,6 +114,9 @@ class CpuEngine:
         oracle.sgd_pass(self.u_host, self.i_host, self.r_host, self.global_mean,
                         self.bu.numpy(), bi, self.P.numpy(), Q, lr=lr, reg=reg, order=order)
 
+    def sse_join(self):
+        pass
+
     def sse_async(self, slot):
         self.sse_buf[slot] = oracle.sse(self.u_host, self.i_host, self.r_host,
                                         self.global_mean, self.bu.numpy(), self.bi.numpy(),

@@ -200,12 +200,14 @@ def test_deep_pipe_equals_per_stratum_launches(dtype, B, kernel, k, nu, ni):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("kernel,k", [("sigmoid", 32), ("linear", 64), ("rbf", 16)])
-def test_eight_wave_kernels(kernel, k):
-    """The 8-wave strata kernels (plans of half the slots, FP32, k <= 64):
-    the persistent epoch is bit-identical to per-stratum launches, and both
-    are the oracle's sequential sweep in the plan's serial order (FP32 vs
-    FP64: train RMSE within 1e-5)."""
+@pytest.mark.parametrize("kernel,k,waves", [("sigmoid", 32, 8), ("linear", 64, 8), ("rbf", 16, 8),
+                                           ("sigmoid", 32, 4), ("linear", 16, 4)])
+def test_eight_wave_kernels(kernel, k, waves):
+    """The 8-wave strata kernels (plans of half the slots, FP32, k <= 64) and
+    their narrow 4-wave form (the same plan, lane groups half as wide,
+    MF_FLAG_NARROW): the persistent epoch is bit-identical to per-stratum
+    launches, and both are the oracle's sequential sweep in the plan's
+    serial order (FP32 vs FP64: train RMSE within 1e-5)."""
     import oracle
 
     nu, ni, nnz = 3000, 800, 120000
@@ -216,9 +218,10 @@ def test_eight_wave_kernels(kernel, k):
     out = []
     for persistent in (True, False):
         eng = _engine(u, i, r, nu, ni, k, kernel, "float32", P, Q, bu, bi)
-        plan = eng.prepare_strata(n_blocks=6, waves=8)
+        plan = eng.prepare_strata(n_blocks=6, waves=waves)
         from matrix_factorization.engine import strata_slots
-        assert plan.NS == strata_slots(k, eng.dcode, 8) == strata_slots(k, eng.dcode) // 2
+        assert plan.NS == strata_slots(k, eng.dcode, waves) == strata_slots(k, eng.dcode) // 2
+        assert plan.narrow == (waves == 4)
         orders = []
         for ep in range(2):
             seq = np.random.RandomState(ep).permutation(6).astype(np.int32)
