@@ -247,11 +247,13 @@ def run_topk(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
     """recommend() for many users at C3 scale.  One step =
     one recommend_batch pass: the top-10 of all n_items for 10K query users
     with their rated items excluded (recommender_base.py:214-271 per user),
-    engine.topk -> mf_topk (score keys + exclusion + radix select), host
-    transfers of the query ids, exclusion CSR and results included.
+    engine.topk_launch with the query ids and the exclusion CSR resident in
+    HBM and the results left there: mf_topk_mm (MFMA candidate filter +
+    exact rescoring) where supported, else mf_topk.
 
-    value = scores/s (query users x items per second).  roofline: HBM at
-    4k B per score (the item row each score reads when nothing is reused)."""
+    value = scores/s (query users x items per second).  roofline: MFMA at
+    2k flops per score for the MFMA filter, else HBM at 4k B per score (the
+    item row each score reads when nothing is reused)."""
     import torch
 
     from matrix_factorization.engine import SGDEngine
@@ -306,24 +308,45 @@ def run_topk(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
         eng.topk_launch(batch)
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    mm = bool(batch["mm"])
+    fallback = eng.topk_finish(batch)      # an overflowed filter re-runs exactly (untimed)
+    if mm:
+        # the whole batch against the exact kernels (untimed): same ids, same scores
+        got_i, got_s = batch["items"].clone(), batch["scores"].clone()
+        eng.topk_launch(batch, exact=True)
+        same = (torch.equal(got_i, batch["items"]) and
+                torch.equal(torch.nan_to_num(got_s, nan=-7.0),
+                            torch.nan_to_num(batch["scores"], nan=-7.0)))
+        parity = dict(parity or {})
+        parity["mfma_filter_equals_exact"] = {"users": n_query, "ids_and_scores_equal": bool(same),
+                                              "overflow_fallback": bool(fallback)}
     scores = n_query * ni * args.steps
     ts = 4 if args.dtype == "float32" else 8
     achieved = scores * k * ts / elapsed / 1e9
+    path = ("MFMA filter (k_topk_mm + k_topk_mm_merge, exact rescoring)" if mm else
+            "two-stage (keys in HBM)" if os.environ.get("MF_TOPK_TWO_STAGE") == "1"
+            else "fused (k_topk_fused + k_topk_merge)")
+    if mm:
+        tf = scores * 2 * k / elapsed / 1e12
+        roof = {"bound": "mfma", "achieved": tf, "peak": 157.3, "unit": "TFLOP/s",
+                "frac": tf / 157.3, "traffic": None, "kernel": "k_topk_mm",
+                "note": "2k flops per score on v_mfma_f32_32x32x2_f32 (f32 MFMA peak); device "
+                        "time of the mf_topk_mm launches (inputs resident) incl. the merge"}
+    else:
+        roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "kernel": "k_topk_fused" if "fused" in path else "k_topk_scores + k_topk_select",
+                "note": "4k B per score (one item row per score, no reuse); device "
+                        "time of the mf_topk launches (inputs resident)"}
     out = {
-        "metric": "top-k scores/s (recommend_batch, mf_topk)", "value": scores / elapsed,
+        "metric": "top-k scores/s (recommend_batch)", "value": scores / elapsed,
         "unit": "scores/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "strong",
         "vs_baseline": None, "dtype": "f32" if ts == 4 else "f64", "data": "synthetic",
         "config": {"workload": desc, "n_users": nu, "n_items": ni, "n_factors": k,
                    "n_query": n_query, "amount": amount, "excluded_pairs": int(ex_ptr[-1]),
-                   "chunk_users": batch["chunk"],
-                   "path": "two-stage (keys in HBM)" if os.environ.get("MF_TOPK_TWO_STAGE") == "1"
-                           else "fused (k_topk_fused + k_topk_merge)"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_topk_scores + k_topk_select",
-                     "note": "4k B per score (one item row per score, no reuse); device "
-                             "time of the mf_topk launches (inputs resident)"},
+                   "chunk_users": batch["chunk"], "path": path},
+        "roofline": roof,
         "cpu_baseline": cpu_baseline, "parity": parity,
     }
     print(json.dumps(out), flush=True)

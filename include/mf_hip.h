@@ -284,6 +284,30 @@ int mf_topk(const int32_t* query_users, int32_t n_query, double global_mean,
             int32_t amount, void* workspace,
             int32_t* out_items, void* out_scores, void* stream);
 
+/*
+ * The same top-k through an MFMA filter (linear kernel, float32, n_factors a
+ * multiple of 4 in [4, 64], 1 <= amount <= 64: mf_topk_mm_supported): scores
+ * of 64-user x 32-item tiles on v_mfma_f32_32x32x2_f32 (another summation
+ * order than predict) only select candidates -- every item whose exact score
+ * can reach the top `amount` within a per-user error bound -- which are then
+ * rescored with predict's arithmetic and ranked exactly as mf_topk ranks
+ * them.  *overflow (device int32, the caller zeroes it) is OR-ed with 1 when
+ * a candidate band outgrew its list (masses of near-equal scores): the
+ * results are then not guaranteed and the caller re-runs mf_topk.  Items
+ * whose score is NaN are never candidates here (mf_topk ranks them last).
+ * workspace: device, >= mf_topk_mm_workspace_bytes(n_query, n_items).
+ */
+int32_t mf_topk_mm_supported(int32_t n_factors, int32_t kernel, int32_t dtype,
+                             int32_t amount);
+size_t mf_topk_mm_workspace_bytes(int32_t n_query, int32_t n_items);
+int mf_topk_mm(const int32_t* query_users, int32_t n_query, double global_mean,
+               const void* user_biases, const void* item_biases,
+               const void* user_features, const void* item_features,
+               int32_t n_items, int32_t n_factors, int32_t kernel, int32_t dtype,
+               const int64_t* exclude_ptr, const int32_t* exclude_items,
+               int32_t amount, void* workspace, int32_t* out_items,
+               void* out_scores, int32_t* overflow, void* stream);
+
 /* ---------------- BaselineModel (bias-only), baseline_model.py ---------- */
 
 /* One bias-SGD epoch over a conflict-free batch schedule: replaces one epoch

@@ -468,6 +468,397 @@ inline bool topk_fused(int32_t amount) {
     return amount <= kFusedMaxAmount && !(e && std::atoi(e) == 1);
 }
 
+// ---------------------------------------------------------------- MFMA filter
+// k_topk_mm (linear kernel, FP32, n_factors a multiple of 4 up to 64): the
+// same top-k as k_topk_fused, with the scores of a 64-user x 32-item tile
+// computed on MFMA (v_mfma_f32_32x32x2_f32, the K dimension split so that
+// lane half h walks columns [h SEG, h SEG + SEG) of the rows it holds).
+// Those scores are NOT k_read's bits (another summation order), so they
+// only FILTER: a candidate enters the user's LDS list if its approximate
+// score s' is at least tau - 2M, tau the amount-th best s' so far and M a
+// bound on |s' - s| for this user:
+//   |dot_mfma - dot_tree| <= (k + 8) 2^-24 ||p|| max ||q||   (both orders,
+//   fma chain and tree of rounded products, within gamma_k sum |p_i q_i|),
+//   + the rounding of the three bias additions,
+// doubled for safety.  Every item whose exact score could reach the exact
+// top `amount` stays in the list; k_topk_mm_merge rescores the survivors
+// with k_read's arithmetic (scalar layout, group_sum<GS>) and ranks them by
+// (exact score desc, item id asc).  A list whose band outgrows its capacity
+// sets *overflow: the results are then not guaranteed and the caller runs
+// the exact path (mf_topk).
+constexpr int kMmUsers = 64;             // users per workgroup: two 32-row MFMA tiles
+constexpr int kMmCap = 256;              // list capacity per user and workgroup
+constexpr int kMmChunk = kWavesPerBlock * 32;   // items scored between barriers
+constexpr int kMmMaxK = 64;
+
+struct MmArgs {
+    const int32_t* users; int32_t nq;
+    const float* P; const float* Q; const float* Bu; const float* Bi;
+    int32_t n_items, k, amount, n_splits;
+    float mu;
+    const float* stats;                  // [2]: max ||q_i||, max |b_i| (k_topk_mm_stats)
+    const int64_t* ex_ptr; const int32_t* ex_items;
+    float* part_s; int32_t* part_id;     // [nq][n_splits][kMmCap]
+    int32_t* part_n;                     // [nq][n_splits]
+    float* marg;                         // [nq]: M per user
+    int32_t* overflow;
+};
+
+// max item-row norm and max |b_i| (non-negative floats: integer max of the bits)
+__global__ __launch_bounds__(kBlock) void k_topk_mm_stats(const float* __restrict__ Q,
+                                                          const float* __restrict__ Bi,
+                                                          int32_t n_items, int32_t k,
+                                                          float* stats) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    float nq = 0.f, nb = 0.f;
+    if (i < n_items) {
+        const float* q = Q + i * k;
+        for (int f = 0; f < k; ++f) nq = __builtin_fmaf(q[f], q[f], nq);
+        nq = sqrtf(nq) * 1.0001f;
+        nb = fabsf(Bi[i]);
+    }
+    nq = fmaxf(nq, __shfl_xor(nq, 32, kWave));
+    nb = fmaxf(nb, __shfl_xor(nb, 32, kWave));
+    for (int o = 16; o > 0; o >>= 1) {
+        nq = fmaxf(nq, __shfl_xor(nq, o, kWave));
+        nb = fmaxf(nb, __shfl_xor(nb, o, kWave));
+    }
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        atomicMax(reinterpret_cast<int*>(stats), __float_as_int(nq));
+        atomicMax(reinterpret_cast<int*>(stats) + 1, __float_as_int(nb));
+    }
+}
+
+// (score desc, id asc) bitonic sort of n (power of two) float-keyed entries
+__device__ __forceinline__ void mm_sort(float* sc, int32_t* id, int n, int t) {
+    for (int sz = 2; sz <= n; sz <<= 1) {
+        for (int st = sz >> 1; st > 0; st >>= 1) {
+            for (int x = t; x < n; x += kBlock) {
+                const int y = x ^ st;
+                if (y > x) {
+                    const bool desc = (x & sz) == 0;
+                    const float kx = sc[x], ky = sc[y];
+                    const int32_t ix = id[x], iy = id[y];
+                    const bool xfirst = kx > ky || (kx == ky && ix < iy);
+                    if (desc ? !xfirst : xfirst) {
+                        sc[x] = ky; sc[y] = kx;
+                        id[x] = iy; id[y] = ix;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// One wave sorts a 256-entry list in LDS by (score desc, id asc): bitonic,
+// two compare-exchange pairs per lane and stage, no workgroup barrier (LDS
+// operations of one wave complete in order; the empty asm keeps the compiler
+// from moving a lane's accesses across stages, i.e. from forwarding its own
+// stores where another lane wrote).
+__device__ __forceinline__ void wave_sort256(float* sc, int32_t* id, int lane) {
+    for (int sz = 2; sz <= kMmCap; sz <<= 1) {
+        for (int st = sz >> 1; st > 0; st >>= 1) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int pi = lane + 64 * e;                 // pair index 0..127
+                const int x = (pi / st) * 2 * st + (pi % st), y = x + st;
+                const bool desc = (x & sz) == 0;
+                const float kx = sc[x], ky = sc[y];
+                const int32_t ix = id[x], iy = id[y];
+                const bool xfirst = kx > ky || (kx == ky && ix < iy);
+                if (desc ? !xfirst : xfirst) {
+                    sc[x] = ky; sc[y] = kx;
+                    id[x] = iy; id[y] = ix;
+                }
+            }
+            asm volatile("" ::: "memory");
+        }
+    }
+}
+
+// One wave compacts user m's list: excluded entries dropped (binary search
+// per entry, in parallel), sorted, cut to the band s' >= (amount-th best) -
+// 2M.  Returns the band size; *adm receives the new admission bound when the
+// list holds at least `amount` entries.
+__device__ __forceinline__ int wave_compact(const MmArgs& A, float* sc, int32_t* id, int n,
+                                            int qy, float mg, int lane, float* adm) {
+    for (int y = lane; y < kMmCap; y += kWave) {
+        float v = -INFINITY;
+        int32_t it = 0x7fffffff;
+        if (y < n) {
+            v = sc[y];
+            it = id[y];
+            if (excluded(A.ex_ptr, A.ex_items, qy, it)) { v = -INFINITY; it = 0x7fffffff; }
+        }
+        sc[y] = v;
+        id[y] = it;
+    }
+    asm volatile("" ::: "memory");
+    wave_sort256(sc, id, lane);
+    int valid = 0, keep = 0;
+    float bound = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < kMmCap / kWave; ++e)
+        valid += __popcll(__ballot(sc[lane + 64 * e] != -INFINITY));
+    if (valid >= A.amount) bound = sc[A.amount - 1] - 2.f * mg;
+#pragma unroll
+    for (int e = 0; e < kMmCap / kWave; ++e)
+        keep += __popcll(__ballot(sc[lane + 64 * e] != -INFINITY && sc[lane + 64 * e] >= bound));
+    *adm = bound;
+    return keep;
+}
+
+template <int SEG>
+__global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    __shared__ float s_sc[kMmUsers][kMmCap];
+    __shared__ int32_t s_id[kMmUsers][kMmCap];
+    __shared__ int s_cnt[kMmUsers];
+    __shared__ float s_adm[kMmUsers];    // admission bound tau - 2M (-inf until a full list)
+    __shared__ float s_bu[kMmUsers];
+    __shared__ float s_m[kMmUsers];
+    __shared__ int s_need, s_lost;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    const int c = lane & 31, h = lane >> 5;
+    const int split = blockIdx.x, q0 = blockIdx.y * kMmUsers;
+    const int k = A.k;
+    const int64_t span = ((int64_t)A.n_items + A.n_splits - 1) / A.n_splits;
+    const int ibeg = (int)min((int64_t)A.n_items, span * split);
+    const int iend = (int)min((int64_t)A.n_items, span * (split + 1));
+    const float qmax = A.stats[0], bimax = A.stats[1];
+    const float ck = 2.f * (float)(k + 8) * 0x1p-24f;
+    if (tid < kMmUsers) {
+        const int qy = q0 + tid;
+        const int32_t uu = qy < A.nq ? A.users[qy] : -1;
+        float pn = 0.f;
+        if (uu >= 0)
+            for (int f = 0; f < k; ++f) pn = __builtin_fmaf(A.P[(int64_t)uu * k + f],
+                                                            A.P[(int64_t)uu * k + f], pn);
+        pn = sqrtf(pn) * 1.0001f;
+        const float bu = uu >= 0 ? A.Bu[uu] : 0.f;
+        // dot-order bound + the bias additions' rounding (scores bounded by
+        // |mu| + |b_u| + max|b_i| + ||p|| max||q||), doubled
+        const float mg = ck * pn * qmax +
+                         0x1p-21f * (fabsf(A.mu) + fabsf(bu) + bimax + pn * qmax);
+        s_cnt[tid] = 0;
+        s_adm[tid] = -INFINITY;
+        s_bu[tid] = bu;
+        s_m[tid] = mg;
+        if (split == 0 && qy < A.nq) A.marg[qy] = mg;
+    }
+    if (tid == 0) { s_need = 0; s_lost = 0; }
+    // A operands: lane (c, h) holds user 32 t + c, columns h SEG .. h SEG + SEG-1
+    float a[2][SEG];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+        const int qy = q0 + 32 * t + c;
+        const int32_t uu = qy < A.nq ? A.users[qy] : -1;
+        const float* pr = A.P + (int64_t)(uu >= 0 ? uu : 0) * k;
+#pragma unroll
+        for (int j = 0; j < SEG; j += 4) {
+            const int c0 = h * SEG + j;
+            const float4 v = *reinterpret_cast<const float4*>(pr + (c0 < k ? c0 : 0));
+            const bool ok = uu >= 0 && c0 < k;
+            a[t][j + 0] = ok ? v.x : 0.f; a[t][j + 1] = ok ? v.y : 0.f;
+            a[t][j + 2] = ok ? v.z : 0.f; a[t][j + 3] = ok ? v.w : 0.f;
+        }
+    }
+    __syncthreads();
+    // per-lane copies of the 32 users' b_u and admission bounds (rows of the
+    // accumulators: users 32 t + ra(i, h)); the bounds change only at a
+    // compaction, after which they are re-read
+    float ubu[2][16], uadm[2][16];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+            ubu[t][i] = s_bu[m];
+            uadm[t][i] = -INFINITY;
+        }
+    auto load_b = [&](int it0, float (&b)[SEG], float& bi) __attribute__((always_inline)) {
+        const int n = it0 + c;
+        const bool have = n < iend;
+        const float* qr = A.Q + (int64_t)(have ? n : 0) * k;
+#pragma unroll
+        for (int j = 0; j < SEG; j += 4) {
+            const int c0 = h * SEG + j;
+            const float4 v = *reinterpret_cast<const float4*>(qr + (c0 < k ? c0 : 0));
+            const bool ok = have && c0 < k;
+            b[j + 0] = ok ? v.x : 0.f; b[j + 1] = ok ? v.y : 0.f;
+            b[j + 2] = ok ? v.z : 0.f; b[j + 3] = ok ? v.w : 0.f;
+        }
+        bi = have ? A.Bi[n] : 0.f;
+    };
+    float b[SEG], bi;
+    load_b(ibeg + wv * 32, b, bi);
+    for (int c0 = ibeg; c0 < iend; c0 += kMmChunk) {
+        const int it0 = c0 + wv * 32;
+        f32x16 acc0, acc1;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < SEG; ++s) {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][s], b[s], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][s], b[s], acc1, 0, 0, 0);
+        }
+        const float bic = bi;
+        const bool have = it0 + c < iend;
+        if (c0 + kMmChunk < iend) load_b(it0 + kMmChunk, b, bi);   // next tile in flight
+        // epilogue: admission only (exclusions are checked when a list is
+        // compacted or written: the rare admitted candidates, in parallel)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+                const float sp = ((A.mu + bic) + ubu[t][i]) + (t ? acc1[i] : acc0[i]);
+                if (have && q0 + m < A.nq && sp >= uadm[t][i]) {
+                    const int slot = atomicAdd(&s_cnt[m], 1);
+                    if (slot < kMmCap) {
+                        s_sc[m][slot] = sp;
+                        s_id[m][slot] = it0 + c;
+                    } else {
+                        s_lost = 1;
+                    }
+                    if (slot >= kMmCap - kMmChunk) s_need = 1;
+                }
+            }
+        }
+        __syncthreads();
+        if (s_need) {                                    // uniform: read after the barrier
+            // lists that could not take another chunk: each wave compacts
+            // users m = wv, wv + 4, ...
+            for (int m = wv; m < kMmUsers; m += kWavesPerBlock) {
+                const int n = min(s_cnt[m], kMmCap);
+                if (n <= kMmCap - kMmChunk) continue;    // wave-uniform
+                float adm;
+                int keep = wave_compact(A, s_sc[m], s_id[m], n, q0 + m, s_m[m], lane, &adm);
+                if (keep > kMmCap - kMmChunk) {          // the band does not fit
+                    if (lane == 0) s_lost = 1;
+                    keep = kMmCap - kMmChunk;
+                }
+                if (lane == 0) {
+                    s_cnt[m] = keep;
+                    s_adm[m] = adm;
+                }
+            }
+            __syncthreads();
+            if (tid == 0) s_need = 0;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    uadm[t][i] = s_adm[32 * t + (i & 3) + 8 * (i >> 2) + 4 * h];
+            __syncthreads();
+        }
+    }
+    // final: each wave compacts its users' lists and writes the bands
+    for (int m = wv; m < kMmUsers; m += kWavesPerBlock) {
+        const int qy = q0 + m;
+        if (qy >= A.nq) break;                           // wave-uniform
+        const int n = min(s_cnt[m], kMmCap);
+        float adm;
+        int keep = wave_compact(A, s_sc[m], s_id[m], n, qy, s_m[m], lane, &adm);
+        const int64_t o = ((int64_t)qy * A.n_splits + split) * kMmCap;
+        for (int y = lane; y < keep; y += kWave) {
+            A.part_s[o + y] = s_sc[m][y];
+            A.part_id[o + y] = s_id[m][y];
+        }
+        if (lane == 0) A.part_n[(int64_t)qy * A.n_splits + split] = keep;
+    }
+    __syncthreads();
+    if (tid == 0 && s_lost) atomicOr(A.overflow, 1);
+}
+
+// per user: merge the splits' bands, keep s' >= (amount-th best s') - 2M,
+// rescore those with k_read's arithmetic, rank by (score desc, id asc) --
+// the order keys and the sort of k_topk_merge, so the output is its output
+template <int GS>
+__global__ __launch_bounds__(kBlock) void k_topk_mm_merge(MmArgs A, int32_t* out_items,
+                                                          float* out_scores) {
+    __shared__ float s_sc[4 * kMmCap];
+    __shared__ int32_t s_id[4 * kMmCap];
+    __shared__ uint64_t s_key[4 * kMmCap];
+    __shared__ int s_off[5], s_keep;
+    const int qy = blockIdx.x, tid = threadIdx.x;
+    const int lane = tid & (kWave - 1), wv = tid / kWave;
+    const int ns = A.n_splits;                       // <= 4 (topk_mm_splits)
+    if (tid == 0) {
+        int n = 0;
+        for (int x = 0; x < ns; ++x) { s_off[x] = n; n += A.part_n[(int64_t)qy * ns + x]; }
+        s_off[ns] = n;
+    }
+    __syncthreads();
+    const int n = s_off[ns];
+    int n2 = 1;
+    while (n2 < max(n, 1)) n2 <<= 1;
+    for (int y = tid; y < n2; y += kBlock) {
+        float sc = -INFINITY;
+        int32_t id = 0x7fffffff;
+        if (y < n) {
+            int x = 0;
+            while (y >= s_off[x + 1]) ++x;
+            const int64_t o = ((int64_t)qy * ns + x) * kMmCap + (y - s_off[x]);
+            sc = A.part_s[o];
+            id = A.part_id[o];
+        }
+        s_sc[y] = sc;
+        s_id[y] = id;
+    }
+    __syncthreads();
+    mm_sort(s_sc, s_id, n2, tid);
+    if (tid == 0) {
+        int keep = n;
+        if (n >= A.amount) {
+            const float adm = s_sc[A.amount - 1] - 2.f * A.marg[qy];
+            keep = A.amount;
+            while (keep < n && s_sc[keep] >= adm) ++keep;
+        }
+        s_keep = keep;
+    }
+    __syncthreads();
+    const int keep = s_keep;
+    // exact rescoring: one candidate per group of GS lanes (scalar layout,
+    // lane partial 0 + p_f q_f, group_sum<GS>, predict_one's additions)
+    const int32_t uu = A.users[qy];
+    const float bu = uu >= 0 ? A.Bu[uu] : 0.f;
+    const int k = A.k;
+    const int g = lane / GS, l = lane % GS;
+    constexpr int R = kWave / GS;
+    const float pl = (uu >= 0 && l < k) ? A.P[(int64_t)uu * k + l] : 0.f;
+    for (int y0 = wv * R; y0 < keep; y0 += kWavesPerBlock * R) {
+        const int y = y0 + g;
+        const bool have = y < keep;
+        const int32_t it = have ? s_id[y] : 0;
+        const float ql = (have && l < k) ? A.Q[(int64_t)it * k + l] : 0.f;
+        const float sc = group_sum<GS>(0.f + pl * ql);
+        const float pred = ((A.mu + (have ? A.Bi[it] : 0.f)) + bu) + sc;
+        if (have && l == 0) s_key[y] = order_key((double)pred);
+    }
+    __syncthreads();
+    int k2 = 1;
+    while (k2 < max(keep, 1)) k2 <<= 1;
+    for (int y = keep + tid; y < k2; y += kBlock) { s_key[y] = 0ull; s_id[y] = 0x7fffffff; }
+    __syncthreads();
+    cand_sort(s_key, s_id, k2, tid, kBlock);
+    for (int y = tid; y < A.amount; y += kBlock) {
+        const bool ok = y < keep && s_key[y] != 0ull;
+        out_items[(int64_t)qy * A.amount + y] = ok ? s_id[y] : -1;
+        out_scores[(int64_t)qy * A.amount + y] =
+            ok ? (float)key_score(s_key[y]) : __int_as_float(0x7fc00000);
+    }
+}
+
+inline int topk_mm_splits(int32_t nq, int32_t n_items) {
+    const int64_t blocks_q = ((int64_t)nq + kMmUsers - 1) / kMmUsers;
+    int64_t s = (1024 + blocks_q - 1) / blocks_q;          // ~4 workgroups per CU
+    s = std::min<int64_t>(s, std::max<int64_t>(1, n_items / 2048));
+    s = std::min<int64_t>(s, 4);                            // merge: 4 x kMmCap entries
+    return (int)std::max<int64_t>(1, s);
+}
+
 struct TopkLaunch {
     const int32_t* users; int32_t nq; double mu; const void* bu; const void* bi;
     const void* P; const void* Q; int32_t n_items; int32_t k; double gamma, lo, hi;
@@ -559,4 +950,85 @@ extern "C" int mf_topk(const int32_t* query_users, int32_t n_query, double globa
                  item_features, n_items, n_factors, gamma, min_rating, max_rating, exclude_ptr,
                  exclude_items, amount, workspace, out_items, out_scores, (hipStream_t)stream};
     return dispatch(dtype, n_factors, kernel, L);
+}
+
+// ---------------------------------------------------------------- MFMA filter ABI
+static int mm_seg(int k) { return ((k / 2 + 3) / 4) * 4; }
+
+extern "C" int32_t mf_topk_mm_supported(int32_t n_factors, int32_t kernel, int32_t dtype,
+                                        int32_t amount) {
+    return (dtype == MF_F32 && kernel == MF_LINEAR && n_factors >= 4 && n_factors <= kMmMaxK &&
+            n_factors % 4 == 0 && amount >= 1 && amount <= kFusedMaxAmount) ? 1 : 0;
+}
+
+extern "C" size_t mf_topk_mm_workspace_bytes(int32_t n_query, int32_t n_items) {
+    if (n_query <= 0 || n_items <= 0) return 0;
+    const size_t ns = (size_t)topk_mm_splits(n_query, n_items);
+    return 16 + 4 * (size_t)n_query + 4 * (size_t)n_query * ns +
+           8 * (size_t)n_query * ns * kMmCap;
+}
+
+extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double global_mean,
+                          const void* user_biases, const void* item_biases,
+                          const void* user_features, const void* item_features, int32_t n_items,
+                          int32_t n_factors, int32_t kernel, int32_t dtype,
+                          const int64_t* exclude_ptr, const int32_t* exclude_items,
+                          int32_t amount, void* workspace, int32_t* out_items, void* out_scores,
+                          int32_t* overflow, void* stream) {
+    if (!mf_topk_mm_supported(n_factors, kernel, dtype, amount)) {
+        set_error("mf_topk_mm: linear kernel, float32, n_factors a multiple of 4 in [4, %d], "
+                  "1 <= amount <= %d only (use mf_topk)", kMmMaxK, kFusedMaxAmount);
+        return MF_ERR_INVALID;
+    }
+    if (n_query < 0 || n_items <= 0) {
+        set_error("mf_topk_mm: n_query >= 0 and n_items > 0 required");
+        return MF_ERR_INVALID;
+    }
+    if (n_query == 0) return MF_OK;
+    if (!workspace || !out_items || !out_scores || !query_users || !overflow ||
+        !user_features || !item_features || !user_biases || !item_biases) {
+        set_error("mf_topk_mm: NULL buffer");
+        return MF_ERR_INVALID;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    MmArgs a;
+    a.users = query_users; a.nq = n_query;
+    a.P = (const float*)user_features; a.Q = (const float*)item_features;
+    a.Bu = (const float*)user_biases; a.Bi = (const float*)item_biases;
+    a.n_items = n_items; a.k = n_factors; a.amount = amount;
+    a.n_splits = topk_mm_splits(n_query, n_items);
+    a.mu = (float)global_mean;
+    a.ex_ptr = exclude_items ? exclude_ptr : nullptr; a.ex_items = exclude_items;
+    char* w = (char*)workspace;
+    float* stats = (float*)w;
+    a.stats = stats;
+    a.marg = (float*)(w + 16);
+    a.part_n = (int32_t*)(a.marg + n_query);
+    a.part_s = (float*)(a.part_n + (size_t)n_query * a.n_splits);
+    a.part_id = (int32_t*)(a.part_s + (size_t)n_query * a.n_splits * kMmCap);
+    a.overflow = overflow;
+    MF_HIP_CHECK(hipMemsetAsync(stats, 0, 8, st));
+    hipLaunchKernelGGL(k_topk_mm_stats, dim3((unsigned)((n_items + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, st, a.Q, a.Bi, n_items, n_factors, stats);
+    const dim3 grid((unsigned)a.n_splits, (unsigned)((n_query + kMmUsers - 1) / kMmUsers));
+    switch (mm_seg(n_factors)) {
+        case 4: hipLaunchKernelGGL(k_topk_mm<4>, grid, dim3(kBlock), 0, st, a); break;
+        case 8: hipLaunchKernelGGL(k_topk_mm<8>, grid, dim3(kBlock), 0, st, a); break;
+        case 12: hipLaunchKernelGGL(k_topk_mm<12>, grid, dim3(kBlock), 0, st, a); break;
+        case 16: hipLaunchKernelGGL(k_topk_mm<16>, grid, dim3(kBlock), 0, st, a); break;
+        case 20: hipLaunchKernelGGL(k_topk_mm<20>, grid, dim3(kBlock), 0, st, a); break;
+        case 24: hipLaunchKernelGGL(k_topk_mm<24>, grid, dim3(kBlock), 0, st, a); break;
+        case 28: hipLaunchKernelGGL(k_topk_mm<28>, grid, dim3(kBlock), 0, st, a); break;
+        default: hipLaunchKernelGGL(k_topk_mm<32>, grid, dim3(kBlock), 0, st, a); break;
+    }
+    switch (kpad_of(n_factors)) {
+        case 16: hipLaunchKernelGGL(k_topk_mm_merge<16>, dim3((unsigned)n_query), dim3(kBlock), 0,
+                                    st, a, out_items, (float*)out_scores); break;
+        case 32: hipLaunchKernelGGL(k_topk_mm_merge<32>, dim3((unsigned)n_query), dim3(kBlock), 0,
+                                    st, a, out_items, (float*)out_scores); break;
+        default: hipLaunchKernelGGL(k_topk_mm_merge<64>, dim3((unsigned)n_query), dim3(kBlock), 0,
+                                    st, a, out_items, (float*)out_scores); break;
+    }
+    MF_HIP_CHECK(hipGetLastError());
+    return MF_OK;
 }

@@ -78,6 +78,11 @@ SIGNATURES = {
     "mf_topk": (ctypes.c_int, [
         _P, _I32, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _F64, _F64,
         _F64, _P, _P, _I32, _P, _P, _P, _P]),
+    "mf_topk_mm_supported": (_I32, [_I32, _I32, _I32, _I32]),
+    "mf_topk_mm_workspace_bytes": (ctypes.c_size_t, [_I32, _I32]),
+    "mf_topk_mm": (ctypes.c_int, [
+        _P, _I32, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _P, _P, _I32, _P, _P,
+        _P, _P, _P]),
     "mf_bias_sgd_epoch": (ctypes.c_int, [
         _P, _P, _P, _I64, _P, _P, _I32, _P, _I32, _F64, _P, _P, _I32, _F64, _F64,
         _I32, _I32, _P]),

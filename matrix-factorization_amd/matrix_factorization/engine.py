@@ -738,6 +738,9 @@ class SGDEngine:
     # path, amount > 64: n_query * n_items * 8 B of keys); users beyond this
     # budget go in further launches
     topk_ws_budget = 1 << 30
+    # recommend_batch through the MFMA candidate filter where supported
+    # (mf_topk_mm; env MF_TOPK_MFMA=0 forces the exact kernels)
+    topk_mfma = True
 
     def topk_prepare(self, users: np.ndarray, amount: int,
                      ex_ptr: Optional[np.ndarray] = None,
@@ -765,37 +768,73 @@ class SGDEngine:
             q["ex_ptr"] = to(ex_ptr - ex_ptr[0])
             q["ex_items"] = to(ex_items if len(ex_items) else np.zeros(1, np.int32))
         lib = _lib.load()
-        # users per launch: grid limits, then halve until the workspace fits
-        chunk = min(nq, 65535 if amount > 64 else 1 << 20)
-        while chunk > 1 and lib.mf_topk_workspace_bytes(chunk, self.n_items,
-                                                        amount) > self.topk_ws_budget:
-            chunk = (chunk + 1) // 2
-        q["chunk"] = chunk
-        wsb = lib.mf_topk_workspace_bytes(chunk, self.n_items, amount)
-        q["ws"] = torch.empty(max(wsb, 8), dtype=torch.uint8, device=self.dev)
+        q["mm"] = (self.topk_mfma and os.environ.get("MF_TOPK_MFMA") != "0" and
+                   bool(lib.mf_topk_mm_supported(self.k, self.kcode, self.dcode, amount)))
+        self._topk_workspace(q, q["mm"])
         q["items"] = torch.empty((nq, amount), dtype=torch.int32, device=self.dev)
         q["scores"] = torch.empty((nq, amount), dtype=self.tdt, device=self.dev)
+        q["ovf"] = torch.zeros(1, dtype=torch.int32, device=self.dev)
         return q
 
-    def topk_launch(self, q: dict) -> None:
-        """Enqueue mf_topk for a prepared batch (results stay on the device)."""
+    def _topk_workspace(self, q: dict, mm: bool) -> None:
+        """Users per launch (grid limits, then halved until the workspace fits
+        ``topk_ws_budget``) and the workspace, for the MFMA-filter path
+        (mf_topk_mm) or the exact one (mf_topk)."""
+        lib = _lib.load()
+        nq, amount = q["nq"], q["amount"]
+        need = ((lambda c: lib.mf_topk_mm_workspace_bytes(c, self.n_items)) if mm else
+                (lambda c: lib.mf_topk_workspace_bytes(c, self.n_items, amount)))
+        chunk = min(nq, 65535 if amount > 64 else 1 << 20)
+        while chunk > 1 and need(chunk) > self.topk_ws_budget:
+            chunk = (chunk + 1) // 2
+        q["chunk"] = chunk
+        q["ws"] = torch.empty(max(need(chunk), 8), dtype=torch.uint8, device=self.dev)
+
+    def topk_launch(self, q: dict, exact: bool = False) -> None:
+        """Enqueue the top-k of a prepared batch (results stay on the device):
+        mf_topk_mm where supported (its overflow word in q["ovf"]), else, or
+        with ``exact``, mf_topk."""
         nq, amount = q["nq"], q["amount"]
         if nq == 0 or amount == 0:
             return
+        mm = q["mm"] and not exact
+        if not mm and q.get("mm"):
+            self._topk_workspace(q, False)        # the exact path's workspace
+            q["mm"] = False
         chunk = q["chunk"]
         es_i, es_s = q["items"].element_size(), q["scores"].element_size()
+        if mm:
+            q["ovf"].zero_()
         with torch.cuda.device(self.dev):
             for q0 in range(0, nq, chunk):
                 q1 = min(nq, q0 + chunk)
                 # CSR offsets stay absolute: the chunk's ptr array starts at row q0
                 dp = None if q["ex_ptr"] is None else _VOID(q["ex_ptr"].data_ptr() + 8 * q0)
-                _lib.call("mf_topk", _VOID(q["users"].data_ptr() + 4 * q0), q1 - q0,
-                          self.global_mean, _tp(self.bu), _tp(self.bi), _tp(self.P),
-                          _tp(self.Q), self.n_items, self.k, self.kcode, self.dcode,
-                          self.gamma, self.min_rating, self.max_rating, dp,
-                          _tp(q["ex_items"]), amount, _tp(q["ws"]),
-                          _VOID(q["items"].data_ptr() + es_i * amount * q0),
-                          _VOID(q["scores"].data_ptr() + es_s * amount * q0), self.stream)
+                users = _VOID(q["users"].data_ptr() + 4 * q0)
+                items = _VOID(q["items"].data_ptr() + es_i * amount * q0)
+                scores = _VOID(q["scores"].data_ptr() + es_s * amount * q0)
+                if mm:
+                    _lib.call("mf_topk_mm", users, q1 - q0, self.global_mean, _tp(self.bu),
+                              _tp(self.bi), _tp(self.P), _tp(self.Q), self.n_items, self.k,
+                              self.kcode, self.dcode, dp, _tp(q["ex_items"]), amount,
+                              _tp(q["ws"]), items, scores, _tp(q["ovf"]), self.stream)
+                else:
+                    _lib.call("mf_topk", users, q1 - q0,
+                              self.global_mean, _tp(self.bu), _tp(self.bi), _tp(self.P),
+                              _tp(self.Q), self.n_items, self.k, self.kcode, self.dcode,
+                              self.gamma, self.min_rating, self.max_rating, dp,
+                              _tp(q["ex_items"]), amount, _tp(q["ws"]), items, scores,
+                              self.stream)
+
+    def topk_finish(self, q: dict) -> bool:
+        """After topk_launch: if the MFMA filter overflowed, re-run the exact
+        path (synchronises).  Returns whether it had to."""
+        if not q.get("mm") or q["nq"] == 0 or q["amount"] == 0:
+            return False
+        if int(q["ovf"].item()) == 0:
+            return False
+        self.topk_launch(q, exact=True)
+        return True
 
     def topk(self, users: np.ndarray, amount: int, ex_ptr: Optional[np.ndarray] = None,
              ex_items: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
@@ -808,6 +847,7 @@ class SGDEngine:
             return (np.full((q["nq"], amount), -1, np.int32),
                     np.full((q["nq"], amount), np.nan, np.float64))
         self.topk_launch(q)
+        self.topk_finish(q)
         return q["items"].cpu().numpy(), q["scores"].cpu().numpy().astype(np.float64)
 
 

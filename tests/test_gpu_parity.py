@@ -321,3 +321,67 @@ def test_fit_empty_and_pickle(mf):
     assert isinstance(m2.user_features, np.ndarray)
     T = X.iloc[:20]
     assert m2.predict(T) == m.predict(T)
+
+
+def _topk_engine(k, nu, ni, seed, dup_items=0, zero_users=0):
+    from matrix_factorization.engine import SGDEngine
+
+    rs = np.random.RandomState(seed)
+    P = rs.normal(0, 0.3, (nu, k)).astype(np.float32)
+    Q = rs.normal(0, 0.3, (ni, k)).astype(np.float32)
+    bu = rs.normal(0, 0.1, nu).astype(np.float32)
+    bi = rs.normal(0, 0.1, ni).astype(np.float32)
+    if dup_items:                     # blocks of identical items: exact score ties
+        Q[:dup_items] = Q[0]
+        bi[:dup_items] = bi[0]
+    if zero_users:                    # all-zero rows: every score is mu + b_i + b_u
+        P[:zero_users] = 0.0
+    eng = SGDEngine(np.zeros(0, np.int32), np.zeros(0, np.int32), np.zeros(0), nu, ni, k,
+                    "linear", "float32", "cuda:0", min_rating=1.0, max_rating=5.0,
+                    global_mean=3.5)
+    eng.load_params(P, Q, bu, bi)
+    return eng
+
+
+def _topk_both(eng, users, amount, ex_ptr=None, ex_items=None):
+    q = eng.topk_prepare(users, amount, ex_ptr, ex_items)
+    assert q["mm"], "the MFMA filter should take this case"
+    eng.topk_launch(q)
+    fell_back = eng.topk_finish(q)
+    mi, ms = q["items"].cpu().numpy(), q["scores"].cpu().numpy()
+    eng.topk_launch(q, exact=True)
+    return mi, ms, q["items"].cpu().numpy(), q["scores"].cpu().numpy(), fell_back
+
+
+@pytest.mark.parametrize("k,amount", [(8, 10), (20, 1), (32, 64), (64, 10), (64, 64)])
+def test_topk_mfma_filter_equals_exact(k, amount):
+    """mf_topk_mm (MFMA scores only select candidates; survivors rescored
+    with predict's arithmetic) returns exactly mf_topk's ids and scores:
+    ragged item / user counts, unknown users (-1), CSR exclusions."""
+    nu, ni = 900, 5003
+    eng = _topk_engine(k, nu, ni, 40 + k)
+    rs = np.random.RandomState(k)
+    users = rs.choice(nu, 333, replace=False).astype(np.int32)
+    users[::50] = -1
+    cnt = rs.randint(0, 40, len(users))
+    ex_ptr = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    ex_items = rs.randint(0, ni, ex_ptr[-1]).astype(np.int32)
+    mi, ms, ei, es, _ = _topk_both(eng, users, amount, ex_ptr, ex_items)
+    assert np.array_equal(mi, ei)
+    assert np.array_equal(ms, es)
+    for q in range(len(users)):
+        assert not set(mi[q]) & set(ex_items[ex_ptr[q]:ex_ptr[q + 1]])
+
+
+def test_topk_mfma_filter_ties_and_overflow():
+    """Masses of exactly equal scores (duplicated items, all-zero users):
+    ties keep the lower item id as in mf_topk; where a band outgrows its
+    list the overflow word sends topk() to the exact path, same result."""
+    k, nu, ni = 32, 200, 3000
+    eng = _topk_engine(k, nu, ni, 7, dup_items=700, zero_users=40)
+    users = np.arange(nu, dtype=np.int32)
+    mi, ms, ei, es, _ = _topk_both(eng, users, 64)
+    assert np.array_equal(mi, ei)
+    assert np.array_equal(ms, es)
+    ids, sc = eng.topk(users, 64)
+    assert np.array_equal(ids, ei)
