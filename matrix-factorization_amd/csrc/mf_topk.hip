@@ -281,6 +281,28 @@ __device__ __forceinline__ void cand_sort(uint64_t* key, int32_t* id, int n, int
     }
 }
 
+// is `it` in the sorted id range items[lo, hi)?
+__device__ __forceinline__ bool in_sorted(const int32_t* items, int64_t lo, int64_t hi, int32_t it) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        const int32_t v = items[mid];
+        if (v == it) return true;
+        if (v < it) lo = mid + 1;
+        else hi = mid;
+    }
+    return false;
+}
+// first position in the sorted items[lo, hi) whose id is >= it
+__device__ __forceinline__ int64_t lower_pos(const int32_t* items, int64_t lo, int64_t hi,
+                                             int32_t it) {
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (items[mid] < it) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
 __device__ __forceinline__ bool excluded(const int64_t* ptr, const int32_t* items, int qy,
                                          int32_t it) {
     if (!ptr) return false;
@@ -502,6 +524,7 @@ struct MmArgs {
     int32_t* part_n;                     // [nq][n_splits]
     float* marg;                         // [nq]: M per user
     int32_t* overflow;
+    int32_t defer;                       // light users skip the exclusion search until the end
 };
 
 // max item-row norm and max |b_i| (non-negative floats: integer max of the bits)
@@ -577,31 +600,36 @@ __device__ __forceinline__ void wave_sort256(float* sc, int32_t* id, int lane) {
     }
 }
 
-// One wave compacts user m's list: excluded entries dropped (binary search
-// per entry, in parallel), sorted, cut to the band s' >= (amount-th best) -
-// 2M.  Returns the band size; *adm receives the new admission bound when the
-// list holds at least `amount` entries.
+// One wave compacts a user's list: sorted, cut to the band s' >= tau - 2M.
+// check: excluded entries are dropped first (binary search in the user's
+// sorted exclusion ids that fall in this split's item range, [elo, ehi)),
+// and tau is the amount-th best; otherwise (a light user during the sweep:
+// at most `extra` excluded ids in the range) tau is the (amount + extra)-th
+// best, of which at least `amount` are not excluded.  Returns the band
+// size; *adm receives the admission bound.
 __device__ __forceinline__ int wave_compact(const MmArgs& A, float* sc, int32_t* id, int n,
-                                            int qy, float mg, int lane, float* adm) {
+                                            bool check, int64_t elo, int64_t ehi, int extra,
+                                            float mg, int lane, float* adm) {
     for (int y = lane; y < kMmCap; y += kWave) {
         float v = -INFINITY;
         int32_t it = 0x7fffffff;
         if (y < n) {
             v = sc[y];
             it = id[y];
-            if (excluded(A.ex_ptr, A.ex_items, qy, it)) { v = -INFINITY; it = 0x7fffffff; }
+            if (check && in_sorted(A.ex_items, elo, ehi, it)) { v = -INFINITY; it = 0x7fffffff; }
         }
         sc[y] = v;
         id[y] = it;
     }
     asm volatile("" ::: "memory");
     wave_sort256(sc, id, lane);
+    const int rank = A.amount + (check ? 0 : extra);     // <= kMmCap (caller)
     int valid = 0, keep = 0;
     float bound = -INFINITY;
 #pragma unroll
     for (int e = 0; e < kMmCap / kWave; ++e)
         valid += __popcll(__ballot(sc[lane + 64 * e] != -INFINITY));
-    if (valid >= A.amount) bound = sc[A.amount - 1] - 2.f * mg;
+    if (valid >= rank) bound = sc[rank - 1] - 2.f * mg;
 #pragma unroll
     for (int e = 0; e < kMmCap / kWave; ++e)
         keep += __popcll(__ballot(sc[lane + 64 * e] != -INFINITY && sc[lane + 64 * e] >= bound));
@@ -618,6 +646,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
     __shared__ float s_adm[kMmUsers];    // admission bound tau - 2M (-inf until a full list)
     __shared__ float s_bu[kMmUsers];
     __shared__ float s_m[kMmUsers];
+    __shared__ int64_t s_elo[kMmUsers], s_ehi[kMmUsers];   // exclusion ids in [ibeg, iend)
     __shared__ int s_need, s_lost;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
     const int c = lane & 31, h = lane >> 5;
@@ -646,6 +675,13 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
         s_bu[tid] = bu;
         s_m[tid] = mg;
         if (split == 0 && qy < A.nq) A.marg[qy] = mg;
+        int64_t lo = 0, hi = 0;
+        if (A.ex_ptr && qy < A.nq) {
+            lo = lower_pos(A.ex_items, A.ex_ptr[qy], A.ex_ptr[qy + 1], ibeg);
+            hi = lower_pos(A.ex_items, lo, A.ex_ptr[qy + 1], iend);
+        }
+        s_elo[tid] = lo;
+        s_ehi[tid] = hi;
     }
     if (tid == 0) { s_need = 0; s_lost = 0; }
     // A operands: lane (c, h) holds user 32 t + c, columns h SEG .. h SEG + SEG-1
@@ -675,21 +711,23 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
         for (int i = 0; i < 16; ++i) {
             const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
             ubu[t][i] = s_bu[m];
-            uadm[t][i] = -INFINITY;
+            uadm[t][i] = q0 + m < A.nq ? -INFINITY : INFINITY;   // no query: never admit
         }
+    // B operands: raw loads, never consumed here (a select on the loaded
+    // values would make the compiler wait for the prefetch right away):
+    // items past the range read a valid row and are never admitted, columns
+    // past k meet zero A operands
     auto load_b = [&](int it0, float (&b)[SEG], float& bi) __attribute__((always_inline)) {
         const int n = it0 + c;
-        const bool have = n < iend;
-        const float* qr = A.Q + (int64_t)(have ? n : 0) * k;
+        const int nn = n < iend ? n : ibeg;
+        const float* qr = A.Q + (int64_t)nn * k;
 #pragma unroll
         for (int j = 0; j < SEG; j += 4) {
             const int c0 = h * SEG + j;
             const float4 v = *reinterpret_cast<const float4*>(qr + (c0 < k ? c0 : 0));
-            const bool ok = have && c0 < k;
-            b[j + 0] = ok ? v.x : 0.f; b[j + 1] = ok ? v.y : 0.f;
-            b[j + 2] = ok ? v.z : 0.f; b[j + 3] = ok ? v.w : 0.f;
+            b[j + 0] = v.x; b[j + 1] = v.y; b[j + 2] = v.z; b[j + 3] = v.w;
         }
-        bi = have ? A.Bi[n] : 0.f;
+        bi = A.Bi[nn];
     };
     float b[SEG], bi;
     load_b(ibeg + wv * 32, b, bi);
@@ -707,22 +745,34 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
         const bool have = it0 + c < iend;
         if (c0 + kMmChunk < iend) load_b(it0 + kMmChunk, b, bi);   // next tile in flight
         // epilogue: admission only (exclusions are checked when a list is
-        // compacted or written: the rare admitted candidates, in parallel)
+        // compacted or written: the rare admitted candidates, in parallel).
+        // The compares go into one wave-wide mask first; the per-score
+        // branches run only when some lane admits something.
+        uint64_t any = 0;
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < 2; ++t)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
                 const float sp = ((A.mu + bic) + ubu[t][i]) + (t ? acc1[i] : acc0[i]);
-                if (have && q0 + m < A.nq && sp >= uadm[t][i]) {
-                    const int slot = atomicAdd(&s_cnt[m], 1);
-                    if (slot < kMmCap) {
-                        s_sc[m][slot] = sp;
-                        s_id[m][slot] = it0 + c;
-                    } else {
-                        s_lost = 1;
+                any |= __ballot(have && sp >= uadm[t][i]);
+            }
+        if (any) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    const float sp = ((A.mu + bic) + ubu[t][i]) + (t ? acc1[i] : acc0[i]);
+                    if (have && sp >= uadm[t][i]) {
+                        const int slot = atomicAdd(&s_cnt[m], 1);
+                        if (slot < kMmCap) {
+                            s_sc[m][slot] = sp;
+                            s_id[m][slot] = it0 + c;
+                        } else {
+                            s_lost = 1;
+                        }
+                        if (slot >= kMmCap - kMmChunk) s_need = 1;
                     }
-                    if (slot >= kMmCap - kMmChunk) s_need = 1;
                 }
             }
         }
@@ -733,8 +783,13 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
             for (int m = wv; m < kMmUsers; m += kWavesPerBlock) {
                 const int n = min(s_cnt[m], kMmCap);
                 if (n <= kMmCap - kMmChunk) continue;    // wave-uniform
+                // light users (few excluded ids in this split) skip the
+                // search until the end: tau ranks amount + extra entries
+                const int extra = (int)(s_ehi[m] - s_elo[m]);
+                const bool heavy = !A.defer || A.amount + extra > (kMmCap - kMmChunk) / 2;
                 float adm;
-                int keep = wave_compact(A, s_sc[m], s_id[m], n, q0 + m, s_m[m], lane, &adm);
+                int keep = wave_compact(A, s_sc[m], s_id[m], n, heavy, s_elo[m], s_ehi[m], extra,
+                                        s_m[m], lane, &adm);
                 if (keep > kMmCap - kMmChunk) {          // the band does not fit
                     if (lane == 0) s_lost = 1;
                     keep = kMmCap - kMmChunk;
@@ -749,8 +804,10 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    uadm[t][i] = s_adm[32 * t + (i & 3) + 8 * (i >> 2) + 4 * h];
+                for (int i = 0; i < 16; ++i) {
+                    const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+                    uadm[t][i] = q0 + m < A.nq ? s_adm[m] : INFINITY;
+                }
             __syncthreads();
         }
     }
@@ -760,7 +817,8 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
         if (qy >= A.nq) break;                           // wave-uniform
         const int n = min(s_cnt[m], kMmCap);
         float adm;
-        int keep = wave_compact(A, s_sc[m], s_id[m], n, qy, s_m[m], lane, &adm);
+        int keep = wave_compact(A, s_sc[m], s_id[m], n, true, s_elo[m], s_ehi[m], 0, s_m[m],
+                                lane, &adm);
         const int64_t o = ((int64_t)qy * A.n_splits + split) * kMmCap;
         for (int y = lane; y < keep; y += kWave) {
             A.part_s[o + y] = s_sc[m][y];
@@ -852,8 +910,14 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm_merge(MmArgs A, int32_t* out
 }
 
 inline int topk_mm_splits(int32_t nq, int32_t n_items) {
+    if (const char* e = std::getenv("MF_TOPK_MM_SPLITS")) {      // probes
+        const int v = std::atoi(e);
+        if (v >= 1 && v <= 4) return v;
+    }
     const int64_t blocks_q = ((int64_t)nq + kMmUsers - 1) / kMmUsers;
-    int64_t s = (1024 + blocks_q - 1) / blocks_q;          // ~4 workgroups per CU
+    // one workgroup per CU (LDS): ~1.9 rounds of 256 (C3, 10K users: 3
+    // splits, 5.3 ms; 1 / 2 / 4 splits 5.5 / 6.9 / 6.5 ms, gpurun_out r02z)
+    int64_t s = (480 + blocks_q / 2) / blocks_q;
     s = std::min<int64_t>(s, std::max<int64_t>(1, n_items / 2048));
     s = std::min<int64_t>(s, 4);                            // merge: 4 x kMmCap entries
     return (int)std::max<int64_t>(1, s);
@@ -1007,6 +1071,10 @@ extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double gl
     a.part_s = (float*)(a.part_n + (size_t)n_query * a.n_splits);
     a.part_id = (int32_t*)(a.part_s + (size_t)n_query * a.n_splits * kMmCap);
     a.overflow = overflow;
+    {
+        const char* e = std::getenv("MF_TOPK_MM_DEFER");             // probes
+        a.defer = e ? std::atoi(e) : 0;
+    }
     MF_HIP_CHECK(hipMemsetAsync(stats, 0, 8, st));
     hipLaunchKernelGGL(k_topk_mm_stats, dim3((unsigned)((n_items + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, st, a.Q, a.Bi, n_items, n_factors, stats);
