@@ -119,6 +119,34 @@ struct SliceTab {
     int32_t n;
 };
 
+// The slice a wave walks and its index among the slice's waves.  n <= 8 (or
+// not a multiple of 8): slice b % n.  n = 8 P, P > 1: the grid is cut into P
+// consecutive parts in dispatch order and part p deals slice (b % 8) + 8 p to
+// block b's XCD, so at any time an XCD's L2 serves about one 1/(8 P) item
+// range instead of P of them side by side (the user rows are then read P
+// times per XCD instead of once).
+struct SliceWave {
+    int x;
+    int64_t wv, nw;
+};
+__device__ __forceinline__ SliceWave slice_wave(const SliceTab& SL) {
+    const int64_t bps = gridDim.x / SL.n;
+    SliceWave s;
+    int64_t j;
+    if (SL.n > 8 && SL.n % 8 == 0) {
+        const int64_t per = gridDim.x / (SL.n / 8);      // = 8 bps blocks per part
+        const int64_t ph = blockIdx.x / per, r = blockIdx.x % per;
+        s.x = (int)(r % 8 + 8 * ph);
+        j = r / 8;
+    } else {
+        s.x = blockIdx.x % SL.n;
+        j = blockIdx.x / SL.n;
+    }
+    s.nw = bps * kWavesPerBlock;
+    s.wv = j * kWavesPerBlock + threadIdx.x / kWave;
+    return s;
+}
+
 // kernels.py:21-105.  `s` = group-reduced dot product (linear/sigmoid) or
 // squared distance (rbf).
 template <typename T, int KERN>
@@ -410,10 +438,10 @@ __global__ __launch_bounds__(kBlock) void k_sse_stream(ReadArgs<T> A, SliceTab S
     const int k = A.k;
     const int kv = k / W;
     const Hyper<T> h = A.h;
-    const int x_slice = blockIdx.x % SL.n;
-    const int64_t bps = gridDim.x / SL.n;
-    const int64_t nw_slice = bps * kWavesPerBlock;
-    const int64_t wv = (int64_t)(blockIdx.x / SL.n) * kWavesPerBlock + threadIdx.x / kWave;
+    const SliceWave sw = slice_wave(SL);
+    const int x_slice = sw.x;
+    const int64_t nw_slice = sw.nw;
+    const int64_t wv = sw.wv;
     const int64_t s0 = SL.off[x_slice], len = SL.off[x_slice + 1] - s0;
     const int64_t b0 = s0 + len * wv / nw_slice;
     const int64_t b1 = s0 + len * (wv + 1) / nw_slice;
@@ -504,10 +532,10 @@ __global__ __launch_bounds__(kBlock) void k_sse_owned(ReadArgs<T> A, SliceTab SL
     const int k = A.k;
     const int kv = k / W;
     const Hyper<T> h = A.h;
-    const int x_slice = blockIdx.x % SL.n;
-    const int64_t bps = gridDim.x / SL.n;
-    const int64_t nw_slice = bps * kWavesPerBlock;
-    const int64_t wv = (int64_t)(blockIdx.x / SL.n) * kWavesPerBlock + threadIdx.x / kWave;
+    const SliceWave sw = slice_wave(SL);
+    const int x_slice = sw.x;
+    const int64_t nw_slice = sw.nw;
+    const int64_t wv = sw.wv;
     const int64_t s0 = SL.off[x_slice], len = SL.off[x_slice + 1] - s0;
     const int64_t b0 = s0 + len * wv / nw_slice;
     const int64_t b1 = s0 + len * (wv + 1) / nw_slice;
@@ -644,10 +672,10 @@ __global__ __launch_bounds__(kBlock) void k_sse_pipe(ReadArgs<T> A, SliceTab SL)
     const int k = A.k;
     const int kv = k / W;
     const Hyper<T> h = A.h;
-    const int x_slice = blockIdx.x % SL.n;
-    const int64_t bps = gridDim.x / SL.n;
-    const int64_t nw_slice = bps * kWavesPerBlock;
-    const int64_t wv = (int64_t)(blockIdx.x / SL.n) * kWavesPerBlock + threadIdx.x / kWave;
+    const SliceWave sw = slice_wave(SL);
+    const int x_slice = sw.x;
+    const int64_t nw_slice = sw.nw;
+    const int64_t wv = sw.wv;
     const int64_t s0 = SL.off[x_slice], len = SL.off[x_slice + 1] - s0;
     const int64_t b0 = s0 + len * wv / nw_slice;
     const int64_t b1 = s0 + len * (wv + 1) / nw_slice;
