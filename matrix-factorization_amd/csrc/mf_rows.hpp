@@ -214,7 +214,9 @@ __device__ __forceinline__ void gather_rows(const T* base, const int (&id)[S], i
             if (v * GS + l >= kv) out[x][v] = (VT)(T)0;
 }
 
-template <typename T, int W, int V, int KERN>
+// FUSED: the FP32 SGD form (fused multiply-adds, see sgd_error); the read
+// paths (predict, SSE, top-k) keep the unfused form they are pinned to.
+template <typename T, int W, int V, int KERN, bool FUSED = false>
 __device__ __forceinline__ T lane_partial(const typename VecOf<T, W>::type (&p)[V],
                                           const typename VecOf<T, W>::type (&q)[V]) {
     T s = (T)0;
@@ -225,7 +227,14 @@ __device__ __forceinline__ T lane_partial(const typename VecOf<T, W>::type (&p)[
             T a, b;
             if constexpr (W == 1) { a = p[v]; b = q[v]; }
             else { a = p[v][w]; b = q[v][w]; }
-            if constexpr (KERN == MF_RBF) {
+            if constexpr (FUSED && std::is_same<T, float>::value) {   // FP32 SGD: fused
+                if constexpr (KERN == MF_RBF) {
+                    const T d = a - b;
+                    s = __builtin_fmaf(d, d, s);
+                } else {
+                    s = __builtin_fmaf(a, b, s);
+                }
+            } else if constexpr (KERN == MF_RBF) {
                 const T d = a - b;
                 s = s + d * d;
             } else {
@@ -240,9 +249,33 @@ __device__ __forceinline__ T lane_partial(const typename VecOf<T, W>::type (&p)[
 // expression order as the reference, FP contraction off).  `s` = group-reduced
 // dot product / squared distance; returns the error e and the kernel's
 // derivative factor d (1 for linear).
+//
+// FP32 (the reference computes in FP64, so the FP32 path is already an
+// approximation held to the RMSE tolerance): exp as v_exp_f32 of x log2(e),
+// the sigmoid's reciprocal as v_rcp_f32, and fused multiply-adds in the
+// row updates -- the C2 step is VALU-issue bound and these are ~40 of its
+// ~120 VALU instructions.  FP64 keeps the reference's expression order
+// unfused (-ffp-contract=off).
+__device__ __forceinline__ float fast_exp(float x) {
+    return __builtin_amdgcn_exp2f(x * 1.44269504088896341f);
+}
+
 template <typename T, int KERN>
 __device__ __forceinline__ void sgd_error(T s, T bu, T bi, T r, const Hyper<T> h, T& e, T& d) {
     d = (T)1;
+    if constexpr (std::is_same<T, float>::value && KERN == MF_SIGMOID) {
+        const float lin = ((h.mu + bu) + bi) + s;
+        const float ex = fast_exp(-lin);
+        const float sg = __builtin_amdgcn_rcpf(1.0f + ex);
+        e = __builtin_fmaf(h.c, sg, h.a) - r;
+        d = (sg * sg) * ex;
+        return;
+    } else if constexpr (std::is_same<T, float>::value && KERN == MF_RBF) {
+        const float E = fast_exp((-h.gamma) * s);
+        e = __builtin_fmaf(h.c, E, h.a) - r;
+        d = (2.0f * E) * h.gamma;
+        return;
+    }
     if constexpr (KERN == MF_LINEAR) {
         const T pred = ((h.mu + bi) + bu) + s;                   // kernels.py:148-153
         e = pred - r;                                            // :156
@@ -264,6 +297,11 @@ __device__ __forceinline__ void sgd_error(T s, T bu, T bi, T r, const Hyper<T> h
 // kernels.py:159-163 (linear) / :239-245 (sigmoid); rbf has no biases
 template <typename T, int KERN>
 __device__ __forceinline__ T sgd_bias(T b, T e, T d, const Hyper<T> h) {
+    if constexpr (std::is_same<T, float>::value) {
+        const float g = KERN == MF_LINEAR ? __builtin_fmaf(h.reg, b, e)
+                                          : __builtin_fmaf(e, d, h.reg * b);
+        return __builtin_fmaf(-h.lr, g, b);
+    }
     if constexpr (KERN == MF_LINEAR) return b - h.lr * (e + h.reg * b);
     else return b - h.lr * (e * d + h.reg * b);
 }
@@ -271,6 +309,20 @@ __device__ __forceinline__ T sgd_bias(T b, T e, T d, const Hyper<T> h) {
 // kernels.py:166-178 / :248-260 / :313-325
 template <typename T, int KERN, typename VT>
 __device__ __forceinline__ void sgd_rows(VT pf, VT qf, T e, T d, const Hyper<T> h, VT& np, VT& nq) {
+    if constexpr (std::is_same<T, float>::value) {
+        // packed FP32 FMAs (v_pk_fma_f32 on float2 halves)
+        const float ed = KERN == MF_LINEAR ? e : e * d;
+        const VT nl = (VT)(-h.lr), rg = (VT)h.reg, ev = (VT)ed;
+        if constexpr (KERN == MF_RBF) {
+            const VT df = qf - pf;
+            np = __builtin_elementwise_fma(nl, __builtin_elementwise_fma(ev, df, rg * pf), pf);
+            nq = __builtin_elementwise_fma(nl, __builtin_elementwise_fma(-ev, df, rg * qf), qf);
+        } else {
+            np = __builtin_elementwise_fma(nl, __builtin_elementwise_fma(ev, qf, rg * pf), pf);
+            nq = __builtin_elementwise_fma(nl, __builtin_elementwise_fma(ev, pf, rg * qf), qf);
+        }
+        return;
+    }
     if constexpr (KERN == MF_LINEAR) {
         np = pf - h.lr * (e * qf + h.reg * pf);
         nq = qf - h.lr * (e * pf + h.reg * qf);
@@ -389,7 +441,7 @@ __global__ __launch_bounds__(kBlock) void k_sgd_batch(SgdArgs<T> A) {
 
 #pragma unroll
     for (int x = 0; x < S; ++x) {
-        const T s = group_sum<GS>(lane_partial<T, W, V, KERN>(p[x], q[x]));
+        const T s = group_sum<GS>(lane_partial<T, W, V, KERN, true>(p[x], q[x]));
         T e, d;
         sgd_error<T, KERN>(s, bu[x], bi[x], rr[x], h, e, d);
         const bool lead = have[x] && l == 0;

@@ -165,7 +165,8 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
     // valid row (first user of the range, slab row 0) and never store.  Row
     // tails past k are masked where the rows are used, not here: a register
     // write would wait for the load in flight.
-    auto unpack_gather = [&](const Tri& tr, Rows& o) __attribute__((always_inline)) {
+    auto unpack_gather = [&](const Tri& tr, Rows& o, auto full) __attribute__((always_inline)) {
+        constexpr bool FULL = decltype(full)::value;
 #pragma unroll
         for (int x = 0; x < S; ++x) {
             const int src = x * R + g;
@@ -182,7 +183,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
 #pragma unroll
             for (int v = 0; v < V; ++v) {
                 const int vi = v * GS + l;
-                const int vc = vi < kv ? vi : kv - 1;                    // kv >= 1
+                const int vc = FULL || vi < kv ? vi : kv - 1;           // kv >= 1
                 if constexpr (WT)   // sc1: L2-served, never a stale L1 line
                     o.p[x][v] = buf_ld<16, VT>(
                         prs, (uint32_t)(((uint32_t)o.u[x] * (uint32_t)k + (uint32_t)(vc * W)) *
@@ -197,10 +198,14 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
 #pragma unroll
     for (int x = 0; x < S; ++x) uprev[x] = -1;
 
-    // step t: triples of t+2 -> trX, rows of t+1 (from trY) -> rwY, apply rwX
-    auto step = [&](int t, Tri& trX, Tri& trY, Rows& rwX, Rows& rwY) __attribute__((always_inline)) {
+    // step t: triples of t+2 -> trX, rows of t+1 (from trY) -> rwY, apply rwX.
+    // full: std::true_type when the lane groups cover the row exactly
+    // (k == GS V W): no tail masks.
+    auto step = [&](int t, Tri& trX, Tri& trY, Rows& rwX, Rows& rwY, auto full)
+                    __attribute__((always_inline)) {
+        constexpr bool FULL = decltype(full)::value;
         load_tri(t + 2, trX);
-        unpack_gather(trY, rwY);
+        unpack_gather(trY, rwY, full);
         VT p[S][V], q[S][V];
         T bu[S], bi[S];
 #pragma unroll
@@ -210,7 +215,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
 #pragma unroll
             for (int v = 0; v < V; ++v) {
                 const int vi = v * GS + l;
-                const bool in = vi < kv;
+                const bool in = FULL || vi < kv;
                 // selects, no branch: the prefetched row is consumed on every
                 // path, so the compiler can wait for exactly that load
                 const VT qv = row[in ? vi : kv - 1];
@@ -226,7 +231,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
         }
 #pragma unroll
         for (int x = 0; x < S; ++x) {
-            const T sm = group_sum<GS>(lane_partial<T, W, V, KERN>(p[x], q[x]));
+            const T sm = group_sum<GS>(lane_partial<T, W, V, KERN, true>(p[x], q[x]));
             T e, d;
             sgd_error<T, KERN>(sm, bu[x], bi[x], rwX.r[x], h, e, d);
             const bool lead = rwX.have[x] && l == 0;
@@ -242,7 +247,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
                 VT np, nq;
                 sgd_rows<T, KERN>(p[x][v], q[x][v], e, d, h, np, nq);
                 pprev[x][v] = np;
-                const bool ok = rwX.have[x] && vi < kv;
+                const bool ok = rwX.have[x] && (FULL || vi < kv);
                 if constexpr (WT) {
                     // unconditional store; a masked lane's offset is out of
                     // range and the store is dropped -- one store per lane and
@@ -270,7 +275,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
     for (int x = 0; x < S; ++x) uprev2[x] = -1;
     // step t (DEPTH 2): rows of t+2 from Tc, triples of t+4 -> Tn, apply Ra
     auto step2 = [&](int t, Tri& Tc, Tri& Tn, Rows& Ra, Rows& Rc) __attribute__((always_inline)) {
-        unpack_gather(Tc, Rc);
+        unpack_gather(Tc, Rc, std::false_type{});
         load_tri(t + 4, Tn);
         VT p[S][V], q[S][V];
         T bu[S], bi[S];
@@ -296,7 +301,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
         }
 #pragma unroll
         for (int x = 0; x < S; ++x) {
-            const T sm = group_sum<GS>(lane_partial<T, W, V, KERN>(p[x], q[x]));
+            const T sm = group_sum<GS>(lane_partial<T, W, V, KERN, true>(p[x], q[x]));
             T e, d;
             sgd_error<T, KERN>(sm, bu[x], bi[x], Ra.r[x], h, e, d);
             const bool lead = Ra.have[x] && l == 0;
@@ -340,13 +345,13 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
             load_tri(0, ta);
             load_tri(1, tb);
             load_tri(2, tc);
-            unpack_gather(ta, ra);
+            unpack_gather(ta, ra, std::false_type{});
             load_tri(3, ta);
-            unpack_gather(tb, rb);
+            unpack_gather(tb, rb, std::false_type{});
         } else {
             load_tri(0, ta);
             load_tri(1, tb);
-            unpack_gather(ta, ra);
+            unpack_gather(ta, ra, std::false_type{});
         }
     }
     if constexpr (BUS_IN && KERN != MF_RBF) {
@@ -394,12 +399,16 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
         if (t < nst) step2(t, tc, tb, ra, rc);
         if (t + 1 < nst) step2(t + 1, ta, tc, rb, ra);
     } else {
-        int t = 0;
-        for (; t + 1 < nst; t += 2) {
-            step(t, ta, tb, ra, rb);
-            step(t + 1, tb, ta, rb, ra);
-        }
-        if (t < nst) step(t, ta, tb, ra, rb);
+        auto sweep = [&](auto full) __attribute__((always_inline)) {
+            int t = 0;
+            for (; t + 1 < nst; t += 2) {
+                step(t, ta, tb, ra, rb, full);
+                step(t + 1, tb, ta, rb, ra, full);
+            }
+            if (t < nst) step(t, ta, tb, ra, rb, full);
+        };
+        if (kv == GS * V) sweep(std::true_type{});
+        else sweep(std::false_type{});
     }
 }
 

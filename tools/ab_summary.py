@@ -1,4 +1,4 @@
-"""Summarise a tools/ab_strata.sh run: SGD / RMSE ms per epoch, prev vs new."""
+"""Summarise an A/B run of tools/gpu.sh bench steps: SGD / RMSE ms per epoch, prev vs new."""
 import glob
 import json
 import os
