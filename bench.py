@@ -580,7 +580,8 @@ def main() -> int:
                       f"({256 if plan.narrow else plan.NS * 1024 // strata_slots(k, eng.dcode)} "
                       f"threads/workgroup{', narrow lane groups' if plan.narrow else ''}) x "
                       f"{int(plan.n_steps.max())} steps max "
-                      f"per block, {fill:.1%} slot fill)")
+                      f"per block, {fill:.1%} slot fill"
+                      f"{', user rows 2 steps ahead' if eng._deep_pipe(plan) else ''})")
     else:
         nb = eng.prepare_colored()
         strat_sizes = np.diff(eng.colored)

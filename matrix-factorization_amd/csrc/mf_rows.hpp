@@ -110,6 +110,9 @@ struct ReadArgs {
     uint64_t p_bytes, q_bytes, bu_bytes, bi_bytes;
 };
 
+// buffer offset past every resource of the read passes: loads return zero
+constexpr uint32_t kBufDropRd = 0xFFFFFFF0u;
+
 // Work split of the read-only passes: `n` slices of the rating array (the
 // item-range slices of mf_sched_slices), slice x walked by the workgroups
 // b with b % n == x.  Placement only changes speed.
@@ -241,6 +244,25 @@ __device__ __forceinline__ T lane_partial(const typename VecOf<T, W>::type (&p)[
                 s = s + a * b;
             }
         }
+    }
+    return s;
+}
+
+// lane_partial of one vector without the leading 0 + (the same value up to
+// the sign of a zero sum): the training-SSE form
+template <typename T, int W, int KERN>
+__device__ __forceinline__ T lane_partial_first(const typename VecOf<T, W>::type (&p)[1],
+                                                const typename VecOf<T, W>::type (&q)[1]) {
+    T s = (T)0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        T a, b;
+        if constexpr (W == 1) { a = p[0]; b = q[0]; }
+        else { a = p[0][w]; b = q[0][w]; }
+        T t;
+        if constexpr (KERN == MF_RBF) { const T d = a - b; t = d * d; }
+        else t = a * b;
+        s = w == 0 ? t : s + t;
     }
     return s;
 }
@@ -700,6 +722,161 @@ __global__ __launch_bounds__(kBlock) void k_sse_owned(ReadArgs<T> A, SliceTab SL
     }
 }
 
+// Training SSE, k_sse_owned's walk with fewer VALU instructions per rating
+// (the pass is VALU-issue bound: 10.4 VALU wave-instructions per rating at
+// C3, PMC r02h, about 1.7 of its 2.3 ms).  Same ratings per wave, same owned
+// user rows, same per-rating arithmetic and the same FP64 sum, bit for bit:
+//  * row offsets as one v_mad_u32_u24 where every id < 2^24 (U24) instead of
+//    the quarter-rate v_mul_lo_u32 + shift;
+//  * the user row and user bias are loaded only inside the wave-uniform
+//    "some group changes user" branch; no zero-fill of skipped slots (their
+//    registers are never selected), one carried row instead of S copies;
+//  * the dot product starts from the first product (0 + x = x up to the
+//    sign of zero, which err^2 does not see); rows without a tail (k ==
+//    GS V W) skip the per-vector masks;
+//  * live ratings counted in int32 per step; the FP64 square-add of FP32
+//    errors as one v_fma_f64 (err^2 is exact in FP64, so fma == mul + add)
+//    of an error zeroed on idle slots and on non-lead lanes.
+template <typename T, int W, int GS, int V, int KERN, int S, bool U24>
+__global__ __launch_bounds__(kBlock) void k_sse_lean(ReadArgs<T> A, SliceTab SL) {
+    using VT = typename VecOf<T, W>::type;
+    constexpr int R = kWave / GS;
+    static_assert(GS % S == 0, "a chunk of GS ratings is whole steps");
+    const int lane = threadIdx.x & (kWave - 1);
+    const int g = lane / GS;
+    const int l = lane % GS;
+    const int k = A.k;
+    const int kv = k / W;
+    const Hyper<T> h = A.h;
+    const SliceWave sw = slice_wave(SL);
+    const int64_t s0 = SL.off[sw.x], len = SL.off[sw.x + 1] - s0;
+    const int64_t b0 = s0 + len * sw.wv / sw.nw;
+    const int64_t b1 = s0 + len * (sw.wv + 1) / sw.nw;
+    double acc = 0.0;
+    if (b0 < b1) {
+        const int64_t wl = b1 - b0;
+        const int64_t r0 = b0 + wl * g / R, r1 = b0 + wl * (g + 1) / R;   // this group's run
+        const int64_t maxrun = (wl + R - 1) / R;                          // wave-uniform trips
+        const int64_t last = r1 > r0 ? r1 - 1 : b0;
+        const int nrun = (int)(r1 - r0);                                  // < 2^31: one wave's share
+        const __amdgpu_buffer_rsrc_t rp = buf_rsrc(A.P, A.p_bytes), rq = buf_rsrc(A.Q, A.q_bytes);
+        const __amdgpu_buffer_rsrc_t rbu = buf_rsrc(A.Bu, A.bu_bytes), rbi = buf_rsrc(A.Bi, A.bi_bytes);
+        const uint32_t kb = (uint32_t)k * (uint32_t)sizeof(T);
+        auto row_off = [&](int id, int vc) __attribute__((always_inline)) -> uint32_t {
+            const uint32_t col = (uint32_t)(vc * W) * (uint32_t)sizeof(T);
+            if constexpr (U24) {
+                // one full-rate instruction; written out because the compiler
+                // turns __umul24 + col into a quarter-rate v_mad_u64_u32 where
+                // it can bound col
+                uint32_t o;
+                asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(o) : "v"(id), "s"(kb), "v"(col));
+                return o;
+            } else {
+                return (uint32_t)id * kb + col;
+            }
+        };
+        const bool lead = l == 0;
+        auto fetch = [&](int64_t c, int& u, int& i, T& r) __attribute__((always_inline)) {
+            const int64_t j = min(r0 + c + l, last);
+            u = A.u[j]; i = A.i[j]; r = A.r[j];
+        };
+        auto sweep = [&](auto full) __attribute__((always_inline)) {
+            constexpr bool FULL = decltype(full)::value;
+            int nu_, ni_;
+            T nr_;
+            fetch(0, nu_, ni_, nr_);
+            int pu = -1;                   // user whose row is carried in pc / buc
+            VT pc[V];
+            T buc = (T)0;
+#pragma unroll
+            for (int v = 0; v < V; ++v) pc[v] = (VT)(T)0;
+            for (int64_t c = 0; c < maxrun; c += GS) {
+                const int tu = nu_, ti = ni_;
+                const T tr = nr_;
+                if (c + GS < maxrun) fetch(c + GS, nu_, ni_, nr_);      // prefetch
+#pragma unroll 1
+                for (int t = 0; t < GS; t += S) {
+                    const int live = nrun - (int)c - t;                 // slots x < live hold a rating
+                    int uu[S], ii[S];
+                    T rr[S];
+                    bool need[S];
+#pragma unroll
+                    for (int x = 0; x < S; ++x) {
+                        const int src = g * GS + t + x;
+                        uu[x] = take_i<GS>(tu, src);
+                        ii[x] = take_i<GS>(ti, src);
+                        rr[x] = take_f<GS>(tr, src);
+                    }
+#pragma unroll
+                    for (int x = 0; x < S; ++x) need[x] = uu[x] != (x == 0 ? pu : uu[x - 1]);
+                    VT q[S][V], pl[S][V];
+                    T bi[S], bul[S];
+#pragma unroll
+                    for (int x = 0; x < S; ++x) {
+#pragma unroll
+                        for (int v = 0; v < V; ++v) {
+                            const int vi = v * GS + l;
+                            const int vc = FULL || vi < kv ? vi : kv - 1;
+                            q[x][v] = buf_ld<0, VT>(rq, row_off(ii[x], vc));
+                        }
+                        if constexpr (KERN != MF_RBF)
+                            bi[x] = buf_ld<0, T>(rbi, (uint32_t)ii[x] * (uint32_t)sizeof(T));
+                        // wave-uniform: skipped unless some group changes user
+                        // here; a lane that keeps its user reads out of range
+                        if (__builtin_amdgcn_ballot_w64(need[x]) != 0) {
+#pragma unroll
+                            for (int v = 0; v < V; ++v) {
+                                const int vi = v * GS + l;
+                                const int vc = FULL || vi < kv ? vi : kv - 1;
+                                pl[x][v] = buf_ld<0, VT>(rp, need[x] ? row_off(uu[x], vc) : kBufDropRd);
+                            }
+                            if constexpr (KERN != MF_RBF)
+                                bul[x] = buf_ld<0, T>(rbu, need[x] ? (uint32_t)uu[x] * (uint32_t)sizeof(T)
+                                                                   : kBufDropRd);
+                        }
+                    }
+#pragma unroll
+                    for (int x = 0; x < S; ++x) {
+                        // the user row of this rating: loaded, or carried
+#pragma unroll
+                        for (int v = 0; v < V; ++v) pc[v] = need[x] ? pl[x][v] : pc[v];
+                        if constexpr (KERN != MF_RBF) buc = need[x] ? bul[x] : buc;
+                        T part = (T)0;
+#pragma unroll
+                        for (int v = 0; v < V; ++v) {
+                            VT pv[1] = {pc[v]}, qv[1] = {q[x][v]};
+                            const T pt = lane_partial_first<T, W, KERN>(pv, qv);
+                            const T ptm = FULL || v * GS + l < kv ? pt : (T)0;
+                            part = v == 0 ? ptm : part + ptm;
+                        }
+                        const T sm = group_sum<GS>(part);
+                        const T err = rr[x] - predict_one<T, KERN>(sm, buc, KERN != MF_RBF ? bi[x] : (T)0, h);
+                        const bool on = (x < live) & lead;     // one select, no branch
+                        const T e = on ? err : (T)0;
+                        if constexpr (std::is_same<T, float>::value)
+                            acc = __builtin_fma((double)e, (double)e, acc);     // e^2 exact in FP64
+                        else
+                            acc += (double)e * (double)e;
+                    }
+                    pu = uu[S - 1];
+                }
+            }
+        };
+        if (kv == GS * V) sweep(std::true_type{});
+        else sweep(std::false_type{});
+    }
+    acc = wave_sum(acc);
+    __shared__ double red[kWavesPerBlock];
+    if (lane == 0) red[threadIdx.x / kWave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+#pragma unroll
+        for (int w = 0; w < kWavesPerBlock; ++w) t += red[w];
+        A.partials[blockIdx.x] = t;
+    }
+}
+
 // Training SSE, software-pipelined form of k_sse_owned (same ratings, same
 // owned user rows, same per-rating arithmetic).  A group's run is cut into
 // chunks of GS ratings (the triples of a chunk arrive in the group's GS
@@ -1055,22 +1232,32 @@ struct SseRun {
         // resource.  Measured at C3 (rank 64, FP32): 2.49 vs 2.66 ms; the
         // owned kernel without the wave-uniform skip of user-row loads took
         // 2.72 ms, with non-temporal user streams 2.69 ms.
+        // k_sse_lean (default; the ids-below-2^24 form where they are) and,
+        // as probes (MF_SSE_VARIANT): 6 = k_sse_owned, the round-2 default.
         const char* ev = std::getenv("MF_SSE_VARIANT");
         int var = ev && std::atoi(ev) == 1 ? 1 : 0;
         if (a.p_bytes >= (1ull << 32) - 64 || a.q_bytes >= (1ull << 32) - 64) var = 1;  // buffer range
+        const bool u24 = p.n_users < (1 << 24) && p.n_items < (1 << 24);
         auto kfn = var == 1 ? k_sse_stream<T, W, GS, V, KERN, S>
-                            : k_sse_owned<T, W, GS, V, KERN, S>;
+                 : u24      ? k_sse_lean<T, W, GS, V, KERN, S, true>
+                            : k_sse_lean<T, W, GS, V, KERN, S, false>;
+        if (var == 0 && ev && std::atoi(ev) == 6) { var = 6; kfn = k_sse_owned<T, W, GS, V, KERN, S>; }
         // FP32 rows of one vector per lane (rank 64): a whole chunk of 16
         // ratings per group per step (C3: 2.45 vs 2.52 ms with S = 4, 2.46
         // with 8; tools/sse_probe.py).  Probes: 2 = 8 per step, 3 = SlotsFor.
         if constexpr (GS == 16 && V == 1 && std::is_same<T, float>::value) {
-            if (var == 0) kfn = k_sse_owned<T, W, GS, V, KERN, 16>;
+            if (var == 0) kfn = u24 ? k_sse_lean<T, W, GS, V, KERN, 16, true>
+                                    : k_sse_lean<T, W, GS, V, KERN, 16, false>;
+            if (var == 6) kfn = k_sse_owned<T, W, GS, V, KERN, 16>;
+            if (var == 0 && u24 && ev && std::atoi(ev) == 8) { var = 8; kfn = k_sse_lean<T, W, GS, V, KERN, 8, true>; }
+            if (var == 0 && u24 && ev && std::atoi(ev) == 9) { var = 9; kfn = k_sse_lean<T, W, GS, V, KERN, 4, true>; }
             if (var == 0 && ev && std::atoi(ev) == 2) { var = 2; kfn = k_sse_owned<T, W, GS, V, KERN, 8>; }
             if (var == 0 && ev && std::atoi(ev) == 3) { var = 3; kfn = k_sse_owned<T, W, GS, V, KERN, S>; }
             if (var == 0 && ev && std::atoi(ev) == 4) { var = 4; kfn = k_sse_pipe<T, W, GS, V, KERN, 8>; }
             if (var == 0 && ev && std::atoi(ev) == 5) { var = 5; kfn = k_sse_pipe<T, W, GS, V, KERN, 4>; }
         }
-        static int resident_tab[6] = {0, 0, 0, 0, 0, 0};   // per instantiation and variant
+        if (var == 0 && !u24) var = 7;                    // its own occupancy entry
+        static int resident_tab[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // per instantiation and variant
         int& resident = resident_tab[var];
         if (resident == 0) {
             int dev = 0, cus = 0, per_cu = 0;

@@ -274,8 +274,10 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
 #pragma unroll
     for (int x = 0; x < S; ++x) uprev2[x] = -1;
     // step t (DEPTH 2): rows of t+2 from Tc, triples of t+4 -> Tn, apply Ra
-    auto step2 = [&](int t, Tri& Tc, Tri& Tn, Rows& Ra, Rows& Rc) __attribute__((always_inline)) {
-        unpack_gather(Tc, Rc, std::false_type{});
+    auto step2 = [&](int t, Tri& Tc, Tri& Tn, Rows& Ra, Rows& Rc, auto full)
+                     __attribute__((always_inline)) {
+        constexpr bool FULL = decltype(full)::value;
+        unpack_gather(Tc, Rc, full);
         load_tri(t + 4, Tn);
         VT p[S][V], q[S][V];
         T bu[S], bi[S];
@@ -287,7 +289,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
 #pragma unroll
             for (int v = 0; v < V; ++v) {
                 const int vi = v * GS + l;
-                const bool in = vi < kv;
+                const bool in = FULL || vi < kv;
                 const VT qv = row[in ? vi : kv - 1];
                 p[x][v] = in ? (f1 ? pprev[x][v] : (f2 ? pprev2[x][v] : Ra.p[x][v])) : (VT)(T)0;
                 q[x][v] = in ? qv : (VT)(T)0;
@@ -318,7 +320,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
                 sgd_rows<T, KERN>(p[x][v], q[x][v], e, d, h, np, nq);
                 pprev2[x][v] = pprev[x][v];
                 pprev[x][v] = np;
-                const bool ok = Ra.have[x] && vi < kv;
+                const bool ok = Ra.have[x] && (FULL || vi < kv);
                 if constexpr (WT) {
                     const uint32_t off = (ok && A.upd_user)
                         ? (uint32_t)(((uint32_t)Ra.u[x] * (uint32_t)k + (uint32_t)(vi * W)) *
@@ -390,14 +392,18 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
     if constexpr (DEPTH == 2) {
         // copies by t mod 3: rows R[t%3] applied at t; triples of t+2 in
         // T[(t+2)%3], the load of t+4 goes to T[(t+1)%3] (consumed at t-1)
-        int t = 0;
-        for (; t + 2 < nst; t += 3) {
-            step2(t, tc, tb, ra, rc);
-            step2(t + 1, ta, tc, rb, ra);
-            step2(t + 2, tb, ta, rc, rb);
-        }
-        if (t < nst) step2(t, tc, tb, ra, rc);
-        if (t + 1 < nst) step2(t + 1, ta, tc, rb, ra);
+        auto sweep2 = [&](auto full) __attribute__((always_inline)) {
+            int t = 0;
+            for (; t + 2 < nst; t += 3) {
+                step2(t, tc, tb, ra, rc, full);
+                step2(t + 1, ta, tc, rb, ra, full);
+                step2(t + 2, tb, ta, rc, rb, full);
+            }
+            if (t < nst) step2(t, tc, tb, ra, rc, full);
+            if (t + 1 < nst) step2(t + 1, ta, tc, rb, ra, full);
+        };
+        if (kv == GS * V) sweep2(std::true_type{});
+        else sweep2(std::false_type{});
     } else {
         auto sweep = [&](auto full) __attribute__((always_inline)) {
             int t = 0;
@@ -749,9 +755,10 @@ struct StrataRun {
         bool persistent = false;
         if ((p.flags & MF_FLAG_PERSISTENT) && p.ws &&
             p.ws_bytes >= strata_ws_bytes(p.B, p.n_seq) && a.p_bytes < (uint64_t)kBufDrop) {
-            // (the deep pipeline exists for 16 waves only)
-            auto efn = (NW == 16 && (p.flags & MF_FLAG_DEEP_PIPE))
-                           ? k_sgd_strata_epoch<T, W, GS, V, KERN, S, NW == 16 ? 2 : 1, NW>
+            // (the deep pipeline exists for the 16- and 8-wave kernels)
+            constexpr int kDeep = NW >= 8 ? 2 : 1;
+            auto efn = (kDeep == 2 && (p.flags & MF_FLAG_DEEP_PIPE))
+                           ? k_sgd_strata_epoch<T, W, GS, V, KERN, S, kDeep, NW>
                            : k_sgd_strata_epoch<T, W, GS, V, KERN, S, 1, NW>;
             MF_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(efn),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

@@ -470,12 +470,20 @@ class SGDEngine:
     strata_deep_pipe: Optional[bool] = None
 
     def _deep_pipe(self, pl) -> bool:
+        """By the plan: on for plans of few busy slots per step (the 8-wave
+        plans, or 16-wave plans filled below 70 %), whose steps wait on the
+        per-CU memory round trip rather than on HBM bandwidth; off for
+        well-filled plans (C3: 9.25 vs 9.43 ms with it; C2 8-wave 0.925 ->
+        0.902 ms, C3 N=8 shard 1.900 -> 1.884 ms)."""
         env = os.environ.get("MF_STRATA_DEEP")
         if env in ("0", "1"):
             return env == "1"
         if self.strata_deep_pipe is not None:
             return bool(self.strata_deep_pipe)
-        return False
+        if pl.narrow:
+            return False                       # no depth-2 form of the 4-wave kernels
+        fill = self.n / max(pl.n_positions, 1)
+        return pl.NS == strata_slots(self.k, self.dcode, 8) or fill < 0.7
 
     def epoch_strata(self, seq: Optional[np.ndarray], seed: int, lr: float, reg: float,
                      update_user: bool = True, update_item: bool = True, timing=False,

@@ -170,13 +170,16 @@ def test_persistent_epoch_equals_per_stratum_launches(dtype, B):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("dtype,B,kernel,k,nu,ni", [
-    ("float64", 6, "linear", 64, 3000, 1200, ),
-    ("float32", 16, "linear", 64, 3000, 1200),
-    ("float32", 8, "sigmoid", 32, 3000, 1200),
-    ("float32", 6, "linear", 64, 200, 2000),      # ~80 ratings per user per block:
-])                                                # rows forwarded from t-1 and t-2
-def test_deep_pipe_equals_per_stratum_launches(dtype, B, kernel, k, nu, ni):
+@pytest.mark.parametrize("dtype,B,kernel,k,nu,ni,waves", [
+    ("float64", 6, "linear", 64, 3000, 1200, None),
+    ("float32", 16, "linear", 64, 3000, 1200, None),
+    ("float32", 8, "sigmoid", 32, 3000, 1200, None),
+    ("float32", 6, "linear", 64, 200, 2000, None),   # ~80 ratings per user per block:
+    ("float32", 8, "sigmoid", 32, 3000, 1200, 8),    # rows forwarded from t-1 and t-2
+    ("float32", 6, "linear", 64, 200, 2000, 8),
+    ("float32", 8, "sigmoid", 20, 3000, 1200, 8),    # row tails (k < GS * V * W)
+])
+def test_deep_pipe_equals_per_stratum_launches(dtype, B, kernel, k, nu, ni, waves):
     """MF_FLAG_DEEP_PIPE (user rows gathered two steps ahead, forwarded from
     either of the two previous steps of the slot) keeps the sequential order:
     bit-identical to one launch per stratum, user-only epochs included."""
@@ -188,7 +191,7 @@ def test_deep_pipe_equals_per_stratum_launches(dtype, B, kernel, k, nu, ni):
     out = []
     for deep in (True, None):
         eng = _engine(u, i, r, nu, ni, k, kernel, dtype, P, Q, bu, bi)
-        eng.prepare_strata(n_blocks=B)
+        eng.prepare_strata(n_blocks=B, waves=waves)
         eng.strata_deep_pipe = deep
         for ep in range(3):
             seq = np.random.RandomState(ep).permutation(B).astype(np.int32)
