@@ -61,7 +61,7 @@ def main():
     cf = known / (f_tot / f_n * 1024.0)
     cw = known / (w_tot / w_n * 1024.0)
     res = {}
-    for name, needle in (("sgd", args.sgd_kernel), ("sse", "k_sse_owned")):
+    for name, needle in (("sgd", args.sgd_kernel), ("sse", "k_sse_")):
         bf, nf = pick(per_kernel(args.bench_fetch, "FETCH_SIZE"), needle)
         bw, nw = pick(per_kernel(args.bench_write, "WRITE_SIZE"), needle)
         res[name] = {
