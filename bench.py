@@ -573,9 +573,12 @@ def main() -> int:
     if strata:
         plan = eng.prepare_strata(n_blocks=args.blocks, waves=args.waves)
         nb = plan.B
+        n_phases = len(getattr(plan, "phases", [plan]))   # item phases (PhasedStrata)
         strat_sizes = plan.stratum_sizes()           # ratings per stratum (launch)
         fill = n_local / max(plan.n_positions, 1)
-        sched_desc = (f"strata (B={nb}: {nb} launches/epoch, item slabs in LDS, "
+        sched_desc = ((f"strata ({n_phases} item phases x B={nb} strata, " if n_phases > 1
+                       else f"strata (B={nb}: {nb} launches/epoch, ")
+                      + "item slabs in LDS, "
                       f"{plan.NS} user-owned slots "
                       f"({256 if plan.narrow else plan.NS * 1024 // strata_slots(k, eng.dcode)} "
                       f"threads/workgroup{', narrow lane groups' if plan.narrow else ''}) x "
@@ -584,6 +587,7 @@ def main() -> int:
                       f"{', user rows 2 steps ahead' if eng._deep_pipe(plan) else ''})")
     else:
         nb = eng.prepare_colored()
+        n_phases = 1
         strat_sizes = np.diff(eng.colored)
         sched_desc = f"colored ({nb} conflict-free batches/epoch on rank 0)"
     t_sched = time.time() - t0
@@ -684,7 +688,7 @@ def main() -> int:
             _, n_launch = run(ep, seq_for(ep), timing=True)
             end()
             eng.sse_async(ep)
-            persistent = n_launch == 1
+            persistent = n_launch == n_phases
             launches_per_epoch = n_launch
         else:
             epoch(ep, False)
@@ -728,7 +732,7 @@ def main() -> int:
             # once per stratum (per-stratum launches)
             slab_passes = 1 if persistent else nb
             alg_epoch = (plan.n_positions * (8 + ts) + n_local * 2 * k * ts
-                         + nb * 2 * n_users_local * ts
+                         + n_phases * nb * 2 * n_users_local * ts
                          + slab_passes * 2 * ni * (k + 1) * ts)
         else:
             alg_epoch = n_local * survey_per_update

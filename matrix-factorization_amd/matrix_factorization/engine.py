@@ -219,6 +219,44 @@ class StrataPlan:
         return np.concatenate(out).astype(np.int64) if out else np.empty(0, np.int64)
 
 
+class PhasedStrata:
+    """Item phases of one strata epoch: the items are cut into P contiguous
+    ranges, and phase p is a whole strata plan over the ratings of range p
+    (item ids relative to its start), run as its own persistent launch on
+    Q / b_i rows [ilo[p], ilo[p+1]).  For item matrices whose slabs would
+    not fit the LDS of one workgroup per CU (C3 at FP64: 52 MB of rows,
+    B = 403 > 256 CUs, i.e. one launch per stratum otherwise), P phases of
+    B <= CUs keep the sweep persistent.  Every phase uses the same B, so an
+    epoch's ``seq`` (a permutation of range(B)) and rotation seed apply to
+    each phase; the sequential order is phase 0's, then phase 1's, ... --
+    again a plain serial order of all the ratings (``serial_order``)."""
+
+    def __init__(self, phases, idx, ilo):
+        self.phases, self.idx = phases, idx
+        self.ilo = np.asarray(ilo, np.int64)
+        self.B, self.NS = phases[0].B, phases[0].NS
+        self.narrow = phases[0].narrow
+        self.max_items = max(pl.max_items for pl in phases)
+        self.max_users = max(pl.max_users for pl in phases)
+
+    @property
+    def n_positions(self) -> int:
+        return sum(pl.n_positions for pl in self.phases)
+
+    @property
+    def n_steps(self) -> np.ndarray:
+        return np.concatenate([pl.n_steps for pl in self.phases])
+
+    def stratum_sizes(self) -> np.ndarray:
+        """Ratings per stratum index, summed over the phases (stratum s of
+        every phase runs when ``seq`` lists s)."""
+        return np.sum([pl.stratum_sizes() for pl in self.phases], axis=0)
+
+    def serial_order(self, seq, seed) -> np.ndarray:
+        parts = [ix[pl.serial_order(seq, seed)] for pl, ix in zip(self.phases, self.idx)]
+        return np.concatenate(parts).astype(np.int64) if parts else np.empty(0, np.int64)
+
+
 def sched_strata(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int, n_blocks: int,
                  ubnd: np.ndarray, ibnd: np.ndarray, n_slots: int):
     """mf_strata_plan_build + fetch: (sched, block step offsets)."""
@@ -415,7 +453,8 @@ class SGDEngine:
         return len(offs) - 1
 
     def prepare_strata(self, n_blocks: Optional[int] = None,
-                       waves: Optional[int] = None) -> "StrataPlan":
+                       waves: Optional[int] = None,
+                       phases: Optional[int] = None) -> "StrataPlan":
         """Build the stratified plan once and store a padded copy of the
         ratings in plan order (block-major, step-major, slot-minor).  The
         host arrays keep the original rating order.
@@ -426,19 +465,67 @@ class SGDEngine:
         than 70 % of its slots (steps bound by the item degree of the
         blocks, not by the slot count), the 8-wave plan is built too and
         kept if steps * waves -- the per-CU VALU issue of an epoch, which
-        bounds such plans (PMC) -- is lower."""
+        bounds such plans (PMC) -- is lower.
+
+        ``phases``: item phases (PhasedStrata).  None = by the plan (env
+        MF_STRATA_PHASES overrides): one phase while the default B fits one
+        workgroup per CU, else the fewest phases whose B does."""
         if self.colored is not None or self.strata is not None:
             raise RuntimeError("ratings already permuted by another schedule")
-        if n_blocks is None:
-            B, ub, ib = choose_strata_blocks(self.u_host, self.i_host, self.n_users,
-                                             self.n_items, self.k, self.dcode)
-        else:
-            B = int(n_blocks)
-            ub = balanced_bounds(self.u_host, self.n_users, B)
-            ib = balanced_bounds(self.i_host, self.n_items, B)
         env = os.environ.get("MF_STRATA_WAVES")
         if waves is None and env in ("4", "8", "16"):
             waves = int(env)
+        if phases is None and os.environ.get("MF_STRATA_PHASES"):
+            phases = int(os.environ["MF_STRATA_PHASES"])
+        if phases is None and n_blocks is None:
+            phases, n_blocks = self._item_phases()
+        if phases is not None and int(phases) > 1:
+            plan = self._prepare_phased(int(phases), n_blocks, waves)
+        else:
+            plan = self._build_plan(self.u_host, self.i_host, self.n_items, n_blocks, waves)
+            plan.to_device(self.u, self.i, self.r, self.dev)
+        self.strata = plan
+        return plan
+
+    def _cus(self) -> int:
+        if self.dev.type != "cuda":
+            return 256
+        return int(torch.cuda.get_device_properties(self.dev).multi_processor_count)
+
+    def _item_phases(self):
+        """(P, B): 1 phase and the default B when the plan's workgroups fit one
+        per CU; else the fewest item phases whose common B does (see
+        PhasedStrata).  B = None: choose_strata_blocks decides."""
+        cus = self._cus()
+        B, _, _ = choose_strata_blocks(self.u_host, self.i_host, self.n_users, self.n_items,
+                                       self.k, self.dcode)
+        if B <= cus or self.n == 0:
+            return 1, B
+        for P in range(2, 9):
+            ilo = balanced_bounds(self.i_host, self.n_items, P)
+            Bp = 0
+            for p in range(P):
+                m = (self.i_host >= ilo[p]) & (self.i_host < ilo[p + 1])
+                b, _, _ = choose_strata_blocks(self.u_host[m], self.i_host[m] - ilo[p],
+                                               self.n_users, int(ilo[p + 1] - ilo[p]),
+                                               self.k, self.dcode, max_blocks=cus)
+                Bp = max(Bp, b)
+            if Bp <= cus:
+                return P, Bp
+        return 1, B                         # no persistent form: one launch per stratum
+
+    def _build_plan(self, u, i, n_items, n_blocks, waves) -> "StrataPlan":
+        if n_blocks is None:
+            B, ub, ib = choose_strata_blocks(u, i, self.n_users, n_items, self.k, self.dcode)
+        else:
+            B = int(n_blocks)
+            ub = balanced_bounds(u, self.n_users, B)
+            ib = balanced_bounds(i, n_items, B)
+            need = _lib.load().mf_strata_lds_bytes(int(np.diff(ib).max()), int(np.diff(ub).max()),
+                                                   self.k, self.dcode)
+            if need > _lib.load().mf_strata_lds_limit():
+                ib = balanced_bounds(i, n_items, B, False)   # equal item counts
+        n = len(u)
         cand = [waves] if waves is not None else [16, 8]
         best = None
         for wv in cand:
@@ -448,19 +535,37 @@ class SGDEngine:
                     raise ValueError(f"no {wv}-wave strata kernel for n_factors={self.k}, "
                                      f"dtype={self.dtype}")
                 continue
-            sched, bstep = sched_strata(self.u_host, self.i_host, self.n_users, self.n_items, B,
-                                        ub, ib, ns)
+            sched, bstep = sched_strata(u, i, self.n_users, n_items, B, ub, ib, ns)
             cost = int(bstep[-1]) * wv
             if best is None or cost < best[0]:
                 best = (cost, ns, sched, bstep)
-            if waves is None and wv == 16 and self.n / max(len(sched), 1) >= 0.7:
+            if waves is None and wv == 16 and n / max(len(sched), 1) >= 0.7:
                 break                       # well filled: the 16-wave plan it is
         _, ns, sched, bstep = best
         plan = StrataPlan(B, ns, ub, ib, bstep, sched)
         plan.narrow = waves == 4
-        plan.to_device(self.u, self.i, self.r, self.dev)
-        self.strata = plan
         return plan
+
+    def _prepare_phased(self, P: int, n_blocks, waves) -> PhasedStrata:
+        ilo = balanced_bounds(self.i_host, self.n_items, P).astype(np.int64)
+        idx = [np.flatnonzero((self.i_host >= ilo[p]) & (self.i_host < ilo[p + 1]))
+               for p in range(P)]
+        if n_blocks is None:                # one B for every phase: the largest needed
+            n_blocks = max(choose_strata_blocks(self.u_host[ix], self.i_host[ix] - ilo[p],
+                                                self.n_users, int(ilo[p + 1] - ilo[p]),
+                                                self.k, self.dcode)[0]
+                           for p, ix in enumerate(idx))
+        plans = []
+        for p, ix in enumerate(idx):
+            ui, ii = self.u_host[ix], self.i_host[ix] - int(ilo[p])
+            pl = self._build_plan(ui, ii, int(ilo[p + 1] - ilo[p]), n_blocks, waves)
+            if waves is None:               # phase 0 picks the kernel shape for all
+                waves = 16 if pl.NS == strata_slots(self.k, self.dcode, 16) else 8
+            t = torch.from_numpy(ix).to(self.dev)
+            pl.to_device(self.u.index_select(0, t), self.i.index_select(0, t) - int(ilo[p]),
+                         self.r.index_select(0, t), self.dev)
+            plans.append(pl)
+        return PhasedStrata(plans, idx, ilo)
 
     # one launch per epoch with the item slabs resident (MF_FLAG_PERSISTENT);
     # False: one launch per stratum
@@ -497,7 +602,16 @@ class SGDEngine:
             raise RuntimeError("call prepare_strata() first")
         seq = (np.arange(pl.B, dtype=np.int32) if seq is None
                else np.ascontiguousarray(seq, np.int32))
+        if isinstance(pl, PhasedStrata):
+            return self._epoch_phased(pl, seq, seed, lr, reg, update_user, update_item, timing,
+                                      persistent, delta)
         ms = (ctypes.c_double * 2)() if timing else None
+        flags = self._strata_flags(pl, persistent)
+        self._run_strata(pl, seq, seed, lr, reg, update_user, update_item, flags, ms, delta,
+                         self.Q, self.bi, self.n_items)
+        return (ms[0], int(ms[1])) if timing else None
+
+    def _strata_flags(self, pl, persistent):
         if persistent is None:
             persistent = self.strata_persistent and os.environ.get("MF_STRATA_PERSISTENT") != "0"
         flags = _lib.MF_FLAG_PERSISTENT if persistent else 0
@@ -507,6 +621,28 @@ class SGDEngine:
             flags |= _lib.MF_FLAG_NO_COOP
         if pl.narrow:
             flags |= _lib.MF_FLAG_NARROW
+        return flags
+
+    def _epoch_phased(self, pl, seq, seed, lr, reg, update_user, update_item, timing,
+                      persistent, delta):
+        """The phases of one epoch in order, each on its rows of Q / b_i (and
+        of the delta buffers)."""
+        flags = self._strata_flags(pl, persistent)
+        tot_ms, launches = 0.0, 0
+        for p, sub in enumerate(pl.phases):
+            lo, hi = int(pl.ilo[p]), int(pl.ilo[p + 1])
+            ms = (ctypes.c_double * 2)() if timing else None
+            d = None if delta is None else (delta[0][lo:hi], delta[1][lo:hi])
+            self._run_strata(sub, seq, seed, lr, reg, update_user, update_item, flags, ms, d,
+                             self.Q[lo:hi], self.bi[lo:hi] if self.bi is not None else None,
+                             hi - lo)
+            if timing:
+                tot_ms += ms[0]
+                launches += int(ms[1])
+        return (tot_ms, launches) if timing else None
+
+    def _run_strata(self, pl, seq, seed, lr, reg, update_user, update_item, flags, ms, delta,
+                    Q, bi, n_items):
         wsb = int(_lib.load().mf_strata_workspace_bytes(pl.B, len(seq)))
         old = getattr(self, "_strata_ws", None)
         if old is None or old.numel() * 4 < wsb:
@@ -520,8 +656,8 @@ class SGDEngine:
         args = (_tp(pl.d_u), _tp(pl.d_i), _tp(pl.d_r),
                 pl.n_positions, pl.B, _tp(pl.d_ubnd), _tp(pl.d_ibnd), _tp(pl.d_bstep),
                 pl.NS, pl.max_items, pl.max_users, _np(seq), len(seq),
-                int(seed) & 0xFFFFFFFF, self.global_mean, _tp(self.bu), _tp(self.bi),
-                _tp(self.P), _tp(self.Q), self.n_users, self.n_items, self.k,
+                int(seed) & 0xFFFFFFFF, self.global_mean, _tp(self.bu), _tp(bi),
+                _tp(self.P), _tp(Q), self.n_users, n_items, self.k,
                 self.kcode, self.dcode, self.gamma, float(lr), float(reg),
                 self.min_rating, self.max_rating, int(update_user), int(update_item),
                 flags, _tp(self._strata_ws), self._strata_ws.numel() * 4)
@@ -531,7 +667,6 @@ class SGDEngine:
             else:
                 _lib.call("mf_sgd_epoch_strata_delta", *args, _tp(delta[0]), _tp(delta[1]),
                           self.stream, ms)
-        return (ms[0], int(ms[1])) if timing else None
 
     def check_strata(self) -> None:
         """Synchronise and raise if a persistent strata sweep gave up waiting

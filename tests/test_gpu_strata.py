@@ -268,3 +268,96 @@ def test_auto_waves_picks_lower_cost():
     seq = np.random.RandomState(0).permutation(B).astype(np.int32)
     eng.epoch_strata(seq, 5, 0.01, 0.02)
     eng.check_strata()
+
+
+@pytest.mark.parametrize("dtype,kernel,k,P,B,waves", [
+    ("float64", "linear", 64, 2, 4, None),
+    ("float64", "sigmoid", 32, 3, 3, None),
+    ("float32", "linear", 64, 2, 6, 8),
+    ("float64", "rbf", 16, 2, 5, None),
+])
+def test_item_phases_equal_serialized_oracle(dtype, kernel, k, P, B, waves):
+    """PhasedStrata: the items cut into P ranges, each a whole strata plan run
+    as its own persistent launch.  The epoch equals the oracle's sweep in
+    plan.serial_order (phase 0's order, then phase 1's, ...), persistent and
+    per-stratum launches are bit-identical, and the delta-out form leaves Q /
+    b_i untouched with the same update in the deltas."""
+    import torch
+
+    import oracle
+    from matrix_factorization.engine import PhasedStrata
+
+    nu, ni, nnz = 3000, 900, 120000
+    u, i, r = _synthetic(31 + P, nu, ni, nnz)
+    rs = np.random.RandomState(32)
+    P0 = rs.normal(0, 0.1, (nu, k)); Q0 = rs.normal(0, 0.1, (ni, k))
+    bu0 = rs.normal(0, 0.1, nu); bi0 = rs.normal(0, 0.1, ni)
+    eps = [(rs.permutation(B).astype(np.int32), int(rs.randint(0, 2**31 - 1))) for _ in range(2)]
+    out = []
+    for persistent in (True, False):
+        eng = _engine(u, i, r, nu, ni, k, kernel, dtype, P0, Q0, bu0, bi0)
+        plan = eng.prepare_strata(n_blocks=B, waves=waves, phases=P)
+        assert isinstance(plan, PhasedStrata) and len(plan.phases) == P and plan.B == B
+        for seq, seed in eps:
+            ms = eng.epoch_strata(seq, seed, lr=0.01, reg=0.02, persistent=persistent,
+                                  timing=True)
+            assert ms[1] == (P if persistent else P * B)
+        eng.check_strata()
+        out.append(eng.params_numpy())
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    hyp = dict(kernel=kernel, gamma=eng.gamma, min_rating=1.0, max_rating=5.0)
+    P2, Q2, bu2, bi2 = P0.copy(), Q0.copy(), bu0.copy(), bi0.copy()
+    for seq, seed in eps:
+        order = plan.serial_order(seq, seed)
+        assert np.array_equal(np.sort(order), np.arange(nnz))
+        oracle.sgd_pass(eng.u_host, eng.i_host, eng.r_host.astype(np.float64), eng.global_mean,
+                        bu2, bi2, P2, Q2, lr=0.01, reg=0.02, order=order, **hyp)
+    tol = 1e-11 if dtype == "float64" else 1e-4
+    for g, o in zip(out[0], (P2, Q2, bu2, bi2)):
+        _close(g, o, tol)
+    # delta-out: the replica stays, the deltas carry the epoch's item update
+    eng = _engine(u, i, r, nu, ni, k, kernel, dtype, P0, Q0, bu0, bi0)
+    eng.prepare_strata(n_blocks=B, waves=waves, phases=P)
+    dq = torch.zeros_like(eng.Q)
+    dbi = torch.zeros_like(eng.bi)
+    seq, seed = eps[0]
+    eng.epoch_strata(seq, seed, lr=0.01, reg=0.02, delta=(dq, dbi))
+    eng.check_strata()
+    Pd, Qd, bud, bid = eng.params_numpy()
+    assert np.array_equal(Qd, Q0.astype(eng.ndt)) and np.array_equal(bid, bi0.astype(eng.ndt))
+    ref = _engine(u, i, r, nu, ni, k, kernel, dtype, P0, Q0, bu0, bi0)
+    ref.prepare_strata(n_blocks=B, waves=waves, phases=P)
+    ref.epoch_strata(seq, seed, lr=0.01, reg=0.02)
+    Pr, Qr, bur, bir = ref.params_numpy()
+    assert np.array_equal(Pd, Pr)
+    _close(Qd + dq.cpu().numpy(), Qr, 1e-12 if dtype == "float64" else 1e-6)
+    if kernel != "rbf":
+        _close(bid + dbi.cpu().numpy(), bir, 1e-12 if dtype == "float64" else 1e-6)
+
+
+def test_item_phases_chosen_when_slabs_exceed_lds():
+    """prepare_strata() picks item phases when the item rows cannot be spread
+    over one workgroup per CU (FP64 rank 128 over 60K items: 62 MB of rows,
+    236 KiB per workgroup at B = 256 > 160 KiB of LDS), and the phased
+    persistent epoch equals its per-stratum launches."""
+    from matrix_factorization.engine import PhasedStrata
+
+    nu, ni, nnz, k = 4000, 60000, 200000, 128
+    u, i, r = _synthetic(41, nu, ni, nnz)
+    rs = np.random.RandomState(42)
+    P0 = rs.normal(0, 0.1, (nu, k)); Q0 = rs.normal(0, 0.1, (ni, k))
+    eng = _engine(u, i, r, nu, ni, k, "linear", "float64", P0, Q0, np.zeros(nu), np.zeros(ni))
+    plan = eng.prepare_strata()
+    assert isinstance(plan, PhasedStrata), "60K items of FP64 rank 128 (62 MB) need phases"
+    assert plan.B <= eng._cus()
+    seq = rs.permutation(plan.B).astype(np.int32)
+    ms = eng.epoch_strata(seq, 5, lr=0.01, reg=0.02, timing=True)
+    assert ms[1] == len(plan.phases)                # persistent: one launch per phase
+    eng.check_strata()
+    got = eng.params_numpy()
+    eng2 = _engine(u, i, r, nu, ni, k, "linear", "float64", P0, Q0, np.zeros(nu), np.zeros(ni))
+    eng2.prepare_strata(n_blocks=plan.B, phases=len(plan.phases))
+    eng2.epoch_strata(seq, 5, lr=0.01, reg=0.02, persistent=False)
+    for a, b in zip(got, eng2.params_numpy()):
+        assert np.array_equal(a, b)
