@@ -477,12 +477,14 @@ class SGDEngine:
             waves = int(env)
         if phases is None and os.environ.get("MF_STRATA_PHASES"):
             phases = int(os.environ["MF_STRATA_PHASES"])
+        bounds = None
         if phases is None and n_blocks is None:
-            phases, n_blocks = self._item_phases()
+            phases, n_blocks, bounds = self._item_phases()
         if phases is not None and int(phases) > 1:
             plan = self._prepare_phased(int(phases), n_blocks, waves)
         else:
-            plan = self._build_plan(self.u_host, self.i_host, self.n_items, n_blocks, waves)
+            plan = self._build_plan(self.u_host, self.i_host, self.n_items, n_blocks, waves,
+                                    bounds)
             plan.to_device(self.u, self.i, self.r, self.dev)
         self.strata = plan
         return plan
@@ -493,14 +495,14 @@ class SGDEngine:
         return int(torch.cuda.get_device_properties(self.dev).multi_processor_count)
 
     def _item_phases(self):
-        """(P, B): 1 phase and the default B when the plan's workgroups fit one
-        per CU; else the fewest item phases whose common B does (see
-        PhasedStrata).  B = None: choose_strata_blocks decides."""
+        """(P, B, bounds): 1 phase and the default B with its user / item
+        bounds when the plan's workgroups fit one per CU; else the fewest item
+        phases whose common B does (see PhasedStrata), bounds None."""
         cus = self._cus()
-        B, _, _ = choose_strata_blocks(self.u_host, self.i_host, self.n_users, self.n_items,
-                                       self.k, self.dcode)
+        B, ub, ib = choose_strata_blocks(self.u_host, self.i_host, self.n_users, self.n_items,
+                                         self.k, self.dcode)
         if B <= cus or self.n == 0:
-            return 1, B
+            return 1, B, (ub, ib)
         for P in range(2, 9):
             ilo = balanced_bounds(self.i_host, self.n_items, P)
             Bp = 0
@@ -511,11 +513,13 @@ class SGDEngine:
                                                self.k, self.dcode, max_blocks=cus)
                 Bp = max(Bp, b)
             if Bp <= cus:
-                return P, Bp
-        return 1, B                         # no persistent form: one launch per stratum
+                return P, Bp, None
+        return 1, B, (ub, ib)               # no persistent form: one launch per stratum
 
-    def _build_plan(self, u, i, n_items, n_blocks, waves) -> "StrataPlan":
-        if n_blocks is None:
+    def _build_plan(self, u, i, n_items, n_blocks, waves, bounds=None) -> "StrataPlan":
+        if bounds is not None:
+            B, (ub, ib) = int(n_blocks), bounds
+        elif n_blocks is None:
             B, ub, ib = choose_strata_blocks(u, i, self.n_users, n_items, self.k, self.dcode)
         else:
             B = int(n_blocks)
