@@ -508,7 +508,6 @@ inline bool topk_fused(int32_t amount) {
 // (exact score desc, item id asc).  A list whose band outgrows its capacity
 // sets *overflow: the results are then not guaranteed and the caller runs
 // the exact path (mf_topk).
-constexpr int kMmUsers = 64;             // users per workgroup: two 32-row MFMA tiles
 constexpr int kMmCap = 256;              // list capacity per user and workgroup
 constexpr int kMmChunk = kWavesPerBlock * 32;   // items scored between barriers
 constexpr int kMmMaxK = 64;
@@ -637,27 +636,31 @@ __device__ __forceinline__ int wave_compact(const MmArgs& A, float* sc, int32_t*
     return keep;
 }
 
-template <int SEG>
+// PIPE: the MFMAs of chunk c+1 are issued before chunk c's admission
+// epilogue (two accumulator pairs), interleaved with it by sched_group_barrier,
+// so the epilogue's VALU work runs in the matrix pipe's shadow.
+template <int SEG, bool PIPE = false, int NT = 2>
 __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
+    constexpr int kU = 32 * NT;          // users per workgroup: NT 32-row MFMA tiles
     using f32x16 = __attribute__((ext_vector_type(16))) float;
-    __shared__ float s_sc[kMmUsers][kMmCap];
-    __shared__ int32_t s_id[kMmUsers][kMmCap];
-    __shared__ int s_cnt[kMmUsers];
-    __shared__ float s_adm[kMmUsers];    // admission bound tau - 2M (-inf until a full list)
-    __shared__ float s_bu[kMmUsers];
-    __shared__ float s_m[kMmUsers];
-    __shared__ int64_t s_elo[kMmUsers], s_ehi[kMmUsers];   // exclusion ids in [ibeg, iend)
+    __shared__ float s_sc[kU][kMmCap];
+    __shared__ int32_t s_id[kU][kMmCap];
+    __shared__ int s_cnt[kU];
+    __shared__ float s_adm[kU];    // admission bound tau - 2M (-inf until a full list)
+    __shared__ float s_bu[kU];
+    __shared__ float s_m[kU];
+    __shared__ int64_t s_elo[kU], s_ehi[kU];   // exclusion ids in [ibeg, iend)
     __shared__ int s_need, s_lost;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
     const int c = lane & 31, h = lane >> 5;
-    const int split = blockIdx.x, q0 = blockIdx.y * kMmUsers;
+    const int split = blockIdx.x, q0 = blockIdx.y * kU;
     const int k = A.k;
     const int64_t span = ((int64_t)A.n_items + A.n_splits - 1) / A.n_splits;
     const int ibeg = (int)min((int64_t)A.n_items, span * split);
     const int iend = (int)min((int64_t)A.n_items, span * (split + 1));
     const float qmax = A.stats[0], bimax = A.stats[1];
     const float ck = 2.f * (float)(k + 8) * 0x1p-24f;
-    if (tid < kMmUsers) {
+    if (tid < kU) {
         const int qy = q0 + tid;
         const int32_t uu = qy < A.nq ? A.users[qy] : -1;
         float pn = 0.f;
@@ -685,9 +688,9 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
     }
     if (tid == 0) { s_need = 0; s_lost = 0; }
     // A operands: lane (c, h) holds user 32 t + c, columns h SEG .. h SEG + SEG-1
-    float a[2][SEG];
+    float a[NT][SEG];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int t = 0; t < NT; ++t) {
         const int qy = q0 + 32 * t + c;
         const int32_t uu = qy < A.nq ? A.users[qy] : -1;
         const float* pr = A.P + (int64_t)(uu >= 0 ? uu : 0) * k;
@@ -704,9 +707,9 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
     // per-lane copies of the 32 users' b_u and admission bounds (rows of the
     // accumulators: users 32 t + ra(i, h)); the bounds change only at a
     // compaction, after which they are re-read
-    float ubu[2][16], uadm[2][16];
+    float ubu[NT][16], uadm[NT][16];
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < NT; ++t)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -721,66 +724,82 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
         const int n = it0 + c;
         const int nn = n < iend ? n : ibeg;
         const float* qr = A.Q + (int64_t)nn * k;
+        bi = A.Bi[nn];                   // first: waiting for it waits for nothing else
 #pragma unroll
         for (int j = 0; j < SEG; j += 4) {
             const int c0 = h * SEG + j;
             const float4 v = *reinterpret_cast<const float4*>(qr + (c0 < k ? c0 : 0));
             b[j + 0] = v.x; b[j + 1] = v.y; b[j + 2] = v.z; b[j + 3] = v.w;
         }
-        bi = A.Bi[nn];
     };
     float b[SEG], bi;
     load_b(ibeg + wv * 32, b, bi);
-    for (int c0 = ibeg; c0 < iend; c0 += kMmChunk) {
+    auto tile = [&](f32x16 (&x)[NT]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[t][i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < SEG; ++s)
+#pragma unroll
+            for (int t = 0; t < NT; ++t)
+                x[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[t][s], b[s], x[t], 0, 0, 0);
+    };
+    // One chunk: MFMA scores of this wave's 32-item tile into acc[NT],
+    // admission of them against the users' bounds.  PIPE: step(c0, X, Y)
+    // runs the admission of chunk c (accumulators X, bias bX) while the
+    // MFMAs of chunk c+1 go into Y -- unconditionally (past the range they
+    // score a clamped valid row that is never admitted), as are the loads of
+    // chunk c+2, so MFMAs, loads and compares share one basic block that the
+    // sched_group_barriers interleave.
+    auto admit = [&](int c0, const f32x16 (&acc)[NT], float bic)
+                     __attribute__((always_inline)) -> uint64_t {
         const int it0 = c0 + wv * 32;
-        f32x16 acc0, acc1;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc0[i] = acc1[i] = 0.f;
-#pragma unroll
-        for (int s = 0; s < SEG; ++s) {
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0][s], b[s], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1][s], b[s], acc1, 0, 0, 0);
-        }
-        const float bic = bi;
         const bool have = it0 + c < iend;
-        if (c0 + kMmChunk < iend) load_b(it0 + kMmChunk, b, bi);   // next tile in flight
         // epilogue: admission only (exclusions are checked when a list is
         // compacted or written: the rare admitted candidates, in parallel).
         // The compares go into one wave-wide mask first; the per-score
         // branches run only when some lane admits something.
         uint64_t any = 0;
 #pragma unroll
-        for (int t = 0; t < 2; ++t)
+        for (int t = 0; t < NT; ++t)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const float sp = ((A.mu + bic) + ubu[t][i]) + (t ? acc1[i] : acc0[i]);
-                any |= __ballot(have && sp >= uadm[t][i]);
+                const float sp = ((A.mu + bic) + ubu[t][i]) + acc[t][i];
+                any |= __builtin_amdgcn_ballot_w64(have && sp >= uadm[t][i]);
             }
-        if (any) {
+        return any;
+    };
+    auto insert = [&](int c0, const f32x16 (&acc)[NT], float bic)
+                      __attribute__((always_inline)) {
+        const int it0 = c0 + wv * 32;
+        const bool have = it0 + c < iend;
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < NT; ++t) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
-                    const float sp = ((A.mu + bic) + ubu[t][i]) + (t ? acc1[i] : acc0[i]);
-                    if (have && sp >= uadm[t][i]) {
-                        const int slot = atomicAdd(&s_cnt[m], 1);
-                        if (slot < kMmCap) {
-                            s_sc[m][slot] = sp;
-                            s_id[m][slot] = it0 + c;
-                        } else {
-                            s_lost = 1;
-                        }
-                        if (slot >= kMmCap - kMmChunk) s_need = 1;
+            for (int i = 0; i < 16; ++i) {
+                const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+                const float sp = ((A.mu + bic) + ubu[t][i]) + acc[t][i];
+                if (have && sp >= uadm[t][i]) {
+                    const int slot = atomicAdd(&s_cnt[m], 1);
+                    if (slot < kMmCap) {
+                        s_sc[m][slot] = sp;
+                        s_id[m][slot] = it0 + c;
+                    } else {
+                        s_lost = 1;
                     }
+                    if (slot >= kMmCap - kMmChunk) s_need = 1;
                 }
             }
         }
+    };
+    // after a chunk's admission: compact the lists that could not take
+    // another chunk (uniform: read after the barrier)
+    auto settle = [&]() __attribute__((always_inline)) {
         __syncthreads();
-        if (s_need) {                                    // uniform: read after the barrier
-            // lists that could not take another chunk: each wave compacts
-            // users m = wv, wv + 4, ...
-            for (int m = wv; m < kMmUsers; m += kWavesPerBlock) {
+        if (s_need) {
+            // each wave compacts users m = wv, wv + 4, ...
+            for (int m = wv; m < kU; m += kWavesPerBlock) {
                 const int n = min(s_cnt[m], kMmCap);
                 if (n <= kMmCap - kMmChunk) continue;    // wave-uniform
                 // light users (few excluded ids in this split) skip the
@@ -802,7 +821,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
             __syncthreads();
             if (tid == 0) s_need = 0;
 #pragma unroll
-            for (int t = 0; t < 2; ++t)
+            for (int t = 0; t < NT; ++t)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
                     const int m = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -810,9 +829,45 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
                 }
             __syncthreads();
         }
+    };
+    if constexpr (PIPE) {
+        f32x16 xa[NT], xb[NT];
+        float ba, bb;
+        tile(xa);                                        // chunk 0
+        ba = bi;
+        load_b(ibeg + kMmChunk + wv * 32, b, bi);        // chunk 1 (clamped past the range)
+        auto step = [&](int c0, f32x16 (&x)[NT], float& bx, f32x16 (&y)[NT], float& by)
+                        __attribute__((always_inline)) {
+            tile(y);                                     // chunk c+1
+            by = bi;
+            load_b(c0 + 2 * kMmChunk + wv * 32, b, bi);  // chunk c+2
+            const uint64_t any = admit(c0, x, bx);
+            // one MFMA, then a share of the compares, ... (0x8 MFMA, 0x2 VALU,
+            // 0x20 VMEM read): the admission runs while the matrix pipe works
+#pragma unroll
+            for (int s = 0; s < NT * SEG; ++s) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+            if (any) insert(c0, x, bx);
+            settle();
+        };
+        for (int c0 = ibeg; c0 < iend; c0 += 2 * kMmChunk) {
+            step(c0, xa, ba, xb, bb);
+            if (c0 + kMmChunk < iend) step(c0 + kMmChunk, xb, bb, xa, ba);
+        }
+    }
+    for (int c0 = ibeg; !PIPE && c0 < iend; c0 += kMmChunk) {
+        f32x16 acc[NT];
+        tile(acc);
+        const float bic = bi;
+        if (c0 + kMmChunk < iend) load_b(c0 + kMmChunk + wv * 32, b, bi);   // next tile in flight
+        if (admit(c0, acc, bic)) insert(c0, acc, bic);
+        settle();
     }
     // final: each wave compacts its users' lists and writes the bands
-    for (int m = wv; m < kMmUsers; m += kWavesPerBlock) {
+    for (int m = wv; m < kU; m += kWavesPerBlock) {
         const int qy = q0 + m;
         if (qy >= A.nq) break;                           // wave-uniform
         const int n = min(s_cnt[m], kMmCap);
@@ -909,15 +964,29 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm_merge(MmArgs A, int32_t* out
     }
 }
 
+// 32-user MFMA tiles per wave of k_topk_mm: 1 (the default: 32 users, 64 KB
+// of lists, 251 VGPRs, two workgroups per CU, so one workgroup's MFMAs run
+// beside the other's admission, barriers and compaction) or 2 (64 users,
+// 128 KB, one workgroup per CU; the round-2 form).  C3, 10K users: 3.55 vs
+// 5.52 ms (gpurun_out r02s14).
+inline int topk_mm_nt() {
+    if (const char* e = std::getenv("MF_TOPK_MM_NT")) {          // probes
+        const int v = std::atoi(e);
+        if (v == 1 || v == 2) return v;
+    }
+    return 1;
+}
+
 inline int topk_mm_splits(int32_t nq, int32_t n_items) {
     if (const char* e = std::getenv("MF_TOPK_MM_SPLITS")) {      // probes
         const int v = std::atoi(e);
         if (v >= 1 && v <= 4) return v;
     }
-    const int64_t blocks_q = ((int64_t)nq + kMmUsers - 1) / kMmUsers;
-    // one workgroup per CU (LDS): ~1.9 rounds of 256 (C3, 10K users: 3
-    // splits, 5.3 ms; 1 / 2 / 4 splits 5.5 / 6.9 / 6.5 ms, gpurun_out r02z)
-    int64_t s = (480 + blocks_q / 2) / blocks_q;
+    const int nt = topk_mm_nt();
+    const int64_t blocks_q = ((int64_t)nq + 32 * nt - 1) / (32 * nt);
+    // ~1.9 rounds of the resident workgroups (one per CU at nt = 2; C3, 10K
+    // users: 3 splits, 5.3 ms; 1 / 2 / 4 splits 5.5 / 6.9 / 6.5 ms, gpurun_out r02z)
+    int64_t s = (480 * (3 - nt) + blocks_q / 2) / blocks_q;
     s = std::min<int64_t>(s, std::max<int64_t>(1, n_items / 2048));
     s = std::min<int64_t>(s, 4);                            // merge: 4 x kMmCap entries
     return (int)std::max<int64_t>(1, s);
@@ -1078,17 +1147,29 @@ extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double gl
     MF_HIP_CHECK(hipMemsetAsync(stats, 0, 8, st));
     hipLaunchKernelGGL(k_topk_mm_stats, dim3((unsigned)((n_items + kBlock - 1) / kBlock)),
                        dim3(kBlock), 0, st, a.Q, a.Bi, n_items, n_factors, stats);
-    const dim3 grid((unsigned)a.n_splits, (unsigned)((n_query + kMmUsers - 1) / kMmUsers));
-    switch (mm_seg(n_factors)) {
-        case 4: hipLaunchKernelGGL(k_topk_mm<4>, grid, dim3(kBlock), 0, st, a); break;
-        case 8: hipLaunchKernelGGL(k_topk_mm<8>, grid, dim3(kBlock), 0, st, a); break;
-        case 12: hipLaunchKernelGGL(k_topk_mm<12>, grid, dim3(kBlock), 0, st, a); break;
-        case 16: hipLaunchKernelGGL(k_topk_mm<16>, grid, dim3(kBlock), 0, st, a); break;
-        case 20: hipLaunchKernelGGL(k_topk_mm<20>, grid, dim3(kBlock), 0, st, a); break;
-        case 24: hipLaunchKernelGGL(k_topk_mm<24>, grid, dim3(kBlock), 0, st, a); break;
-        case 28: hipLaunchKernelGGL(k_topk_mm<28>, grid, dim3(kBlock), 0, st, a); break;
-        default: hipLaunchKernelGGL(k_topk_mm<32>, grid, dim3(kBlock), 0, st, a); break;
+    const int nt = topk_mm_nt();
+    const dim3 grid((unsigned)a.n_splits, (unsigned)((n_query + 32 * nt - 1) / (32 * nt)));
+    const char* pe = std::getenv("MF_TOPK_MM_PIPE");
+    const bool pipe = pe ? std::atoi(pe) != 0 : true;
+#define MF_MM_LAUNCH(S)                                                                        \
+    if (nt == 1) {                                                                            \
+        if (pipe) hipLaunchKernelGGL((k_topk_mm<S, true, 1>), grid, dim3(kBlock), 0, st, a);  \
+        else hipLaunchKernelGGL((k_topk_mm<S, false, 1>), grid, dim3(kBlock), 0, st, a);      \
+    } else {                                                                                  \
+        if (pipe) hipLaunchKernelGGL((k_topk_mm<S, true, 2>), grid, dim3(kBlock), 0, st, a);  \
+        else hipLaunchKernelGGL((k_topk_mm<S, false, 2>), grid, dim3(kBlock), 0, st, a);      \
     }
+    switch (mm_seg(n_factors)) {
+        case 4: MF_MM_LAUNCH(4); break;
+        case 8: MF_MM_LAUNCH(8); break;
+        case 12: MF_MM_LAUNCH(12); break;
+        case 16: MF_MM_LAUNCH(16); break;
+        case 20: MF_MM_LAUNCH(20); break;
+        case 24: MF_MM_LAUNCH(24); break;
+        case 28: MF_MM_LAUNCH(28); break;
+        default: MF_MM_LAUNCH(32); break;
+    }
+#undef MF_MM_LAUNCH
     switch (kpad_of(n_factors)) {
         case 16: hipLaunchKernelGGL(k_topk_mm_merge<16>, dim3((unsigned)n_query), dim3(kBlock), 0,
                                     st, a, out_items, (float*)out_scores); break;
