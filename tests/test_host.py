@@ -436,3 +436,62 @@ def test_strata_serial_order_and_rejections():
     assert E.strata_slots(16, _lib.MF_F32) == 256
     assert E.strata_slots(64, _lib.MF_F64) == 64          # one slot per group (FP64 rows)
     assert _lib.load().mf_strata_slots(-1, 0) == -1
+
+
+def test_phased_strata_host_composition():
+    """PhasedStrata (item phases, host side): the epoch's serial order is the
+    phases' serial orders mapped back to global rating indices, phase 0
+    first; it lists every rating once; stratum sizes add up per stratum."""
+    from matrix_factorization.engine import (PhasedStrata, StrataPlan, balanced_bounds,
+                                             sched_strata)
+
+    rs = np.random.RandomState(5)
+    nu, ni, n, B, NS = 300, 240, 6000, 4, 64
+    keys = rs.choice(nu * ni, n, replace=False)
+    u = (keys // ni).astype(np.int32)
+    i = (keys % ni).astype(np.int32)
+    ilo = balanced_bounds(i, ni, 2).astype(np.int64)
+    plans, idx = [], []
+    for p in range(2):
+        ix = np.flatnonzero((i >= ilo[p]) & (i < ilo[p + 1]))
+        ui, ii = u[ix], i[ix] - int(ilo[p])
+        nip = int(ilo[p + 1] - ilo[p])
+        ub, ib = balanced_bounds(ui, nu, B), balanced_bounds(ii, nip, B)
+        sched, bstep = sched_strata(ui, ii, nu, nip, B, ub, ib, NS)
+        plans.append(StrataPlan(B, NS, ub, ib, bstep, sched))
+        idx.append(ix)
+    ph = PhasedStrata(plans, idx, ilo)
+    seq = np.array([2, 0, 3, 1], np.int32)
+    order = ph.serial_order(seq, 77)
+    assert np.array_equal(np.sort(order), np.arange(n))
+    n0 = len(idx[0])
+    assert np.all(i[order[:n0]] < ilo[1]) and np.all(i[order[n0:]] >= ilo[1])
+    assert np.array_equal(order[:n0], idx[0][plans[0].serial_order(seq, 77)])
+    assert np.array_equal(ph.stratum_sizes(), plans[0].stratum_sizes() + plans[1].stratum_sizes())
+    assert ph.n_positions == plans[0].n_positions + plans[1].n_positions
+    assert ph.B == B and ph.NS == NS
+
+
+def test_deep_pipe_default_by_plan_shape(monkeypatch):
+    """MF_FLAG_DEEP_PIPE by plan shape: on for 8-wave plans and for 16-wave
+    plans filled below 70 %, off for well-filled 16-wave plans and for the
+    narrow kernels; MF_STRATA_DEEP / strata_deep_pipe override."""
+    from types import SimpleNamespace
+
+    from matrix_factorization.engine import SGDEngine, strata_slots
+
+    monkeypatch.delenv("MF_STRATA_DEEP", raising=False)
+    k, dcode = 64, 0
+    ns16, ns8 = strata_slots(k, dcode, 16), strata_slots(k, dcode, 8)
+    eng = SimpleNamespace(n=1000, k=k, dcode=dcode, strata_deep_pipe=None)
+    plan = lambda ns, npos, narrow=False: SimpleNamespace(NS=ns, n_positions=npos,  # noqa: E731
+                                                           narrow=narrow)
+    deep = lambda pl: SGDEngine._deep_pipe(eng, pl)  # noqa: E731
+    assert deep(plan(ns16, 1100)) is False          # 91 % filled
+    assert deep(plan(ns16, 1500)) is True           # 67 % filled
+    assert deep(plan(ns8, 1050)) is True            # 8 waves
+    assert deep(plan(ns8, 1050, narrow=True)) is False
+    eng.strata_deep_pipe = False
+    assert deep(plan(ns8, 1050)) is False
+    monkeypatch.setenv("MF_STRATA_DEEP", "1")
+    assert deep(plan(ns16, 1100)) is True
