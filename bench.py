@@ -689,6 +689,9 @@ def main() -> int:
             end()
             eng.sse_async(ep)
             persistent = n_launch == n_phases
+            if persistent:           # one persistent launch per epoch (per item phase)
+                sched_desc = sched_desc.replace(
+                    f"B={nb}: {nb} launches/epoch", f"B={nb} strata in 1 persistent launch/epoch")
             launches_per_epoch = n_launch
         else:
             epoch(ep, False)
