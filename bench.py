@@ -106,17 +106,21 @@ def synth(n_users: int, n_items: int, nnz: int, seed: int = 20261015):
     return u, i, r
 
 
-def traffic_from_profiles(workload: str, n_gpus: int, schedule: str = "colored"):
-    """HBM bytes per SGD launch measured by rocprofv3 PMC passes, if a
-    summary for this workload was committed under profiles/."""
+def traffic_from_profiles(workload: str, n_gpus: int, schedule: str, dtype: str,
+                          kernel: str):
+    """HBM bytes per SGD launch measured by rocprofv3 PMC passes for exactly
+    this workload, schedule, dtype and kernel, if committed under
+    profiles/traffic.json; else None (the line then says `traffic: null`
+    rather than borrowing another configuration's counters)."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        key = f"{workload}/n{n_gpus}" if schedule == "colored" else f"{workload}/{schedule}/n{n_gpus}"
-        e = d.get(key)
-        return None if e is None else float(e["hbm_bytes_per_sgd_launch"])
-    except (OSError, ValueError, KeyError):
+        e = d.get(f"{workload}/{schedule}/{dtype}/n{n_gpus}")
+        if e is None or e.get("kernel") != kernel:
+            return None
+        return float(e["hbm_bytes_per_sgd_launch"])
+    except (OSError, ValueError, KeyError, AttributeError):
         return None
 
 
@@ -164,13 +168,14 @@ def run_als(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
         log(f"cpu oracle: user half-sweep of {n_s} users = {S} ratings, FP64, 1 thread")
         from threadpoolctl import threadpool_limits
 
-        with threadpool_limits(1):                 # one core, as the SGD leg
+        with threadpool_limits(1), pinned_core() as core:   # one core, as the SGD leg
             t0 = time.perf_counter()
             bo, Po = oracle.als_half_sweep(u[sel], i[sel], r[sel], np.float32(mu),
                                            np.zeros(ni), Q0, n_s, reg)
             t_cpu = time.perf_counter() - t0
         cpu_baseline = {
             "value": S / t_cpu / 2, "unit": "rating-updates/s", "cores": 1, "kind": "port",
+            "affinity": core,
             "sample": (f"user half-sweep of the first {n_s} users ({S} ratings, {t_cpu:.1f}s) "
                        f"of the same workload, oracle.als_half_sweep (NumPy FP64, "
                        f"np.linalg.solve per user); value = ratings / (2 x time), an "
@@ -280,16 +285,18 @@ def run_topk(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
         P64, Q64 = P0.astype(np.float64), Q0.astype(np.float64)
         allq = np.arange(ni, dtype=np.int32)
         ref = []
-        t0 = time.perf_counter()
-        for q in range(ns):
-            # recommend(): predict(bound_ratings=False) of every candidate item,
-            # sort descending (stable: lower item id first among equal scores)
-            pred = oracle.predict(np.full(ni, users[q], np.int32), allq, mu, bu0, bi0, P64, Q64,
-                                  min_rating=1.0, max_rating=5.0, bound=False)
-            pred[ex_items[ex_ptr[q]:ex_ptr[q + 1]]] = -np.inf
-            ref.append(np.argsort(-pred, kind="stable")[:amount])
-        t_cpu = time.perf_counter() - t0
+        with pinned_core() as core:
+            t0 = time.perf_counter()
+            for q in range(ns):
+                # recommend(): predict(bound_ratings=False) of every candidate item,
+                # sort descending (stable: lower item id first among equal scores)
+                pred = oracle.predict(np.full(ni, users[q], np.int32), allq, mu, bu0, bi0, P64,
+                                      Q64, min_rating=1.0, max_rating=5.0, bound=False)
+                pred[ex_items[ex_ptr[q]:ex_ptr[q + 1]]] = -np.inf
+                ref.append(np.argsort(-pred, kind="stable")[:amount])
+            t_cpu = time.perf_counter() - t0
         cpu_baseline = {"value": ns * ni / t_cpu, "unit": "scores/s", "cores": 1, "kind": "port",
+                        "affinity": core,
                         "sample": f"{ns} of the query users: oracle.predict of all {ni} items "
                                   f"(FP64 C restatement of _predict) + stable argsort, one thread",
                         **host_info()}
@@ -371,6 +378,27 @@ def host_info() -> dict:
     return {"cpu_model": model, "nproc": nproc, "os_cpu_count": os.cpu_count()}
 
 
+class pinned_core:
+    """Context manager: the calling thread's CPU affinity set to one core (the
+    lowest of its current set) for the duration; yields a record of the mask
+    actually in force, e.g. {"cpus": [0], "pinned": true}."""
+
+    def __enter__(self):
+        try:
+            self.old = os.sched_getaffinity(0)
+            core = min(self.old)
+            os.sched_setaffinity(0, {core})
+            return {"cpus": sorted(os.sched_getaffinity(0)), "pinned": True}
+        except (AttributeError, OSError) as e:
+            self.old = None
+            return {"cpus": None, "pinned": False, "error": str(e)}
+
+    def __exit__(self, *exc):
+        if self.old is not None:
+            os.sched_setaffinity(0, self.old)
+        return False
+
+
 def cpu_leg(args, eng, run, serial, seq_for, rot_for, reset_params, strat_sizes, nb, strata,
             kernel, k, mu, P0, Q0, nu, ni, n_local):
     """CPU baseline + parity, untimed, before the timed epochs.
@@ -431,7 +459,9 @@ def cpu_leg(args, eng, run, serial, seq_for, rot_for, reset_params, strat_sizes,
 
     log(f"cpu oracle (a): {S} ratings ({m} of {nb} {unit_name}, GPU serial order), FP64, "
         f"1 thread")
-    (bu, bi, P, Q), rm_a, t_sgd, t_sse = epoch(order)
+    # pinned to one core for the timed leg (`taskset -c 0`)
+    with pinned_core() as core:
+        (bu, bi, P, Q), rm_a, t_sgd, t_sse = epoch(order)
     rm_g = float(np.sqrt(oracle.sse(u, i, r, mu, bug, big, Pg, Qg, **hyp) / len(u)))
     host = host_info()
     what = (f"one full epoch (all {S} ratings)" if full
@@ -440,7 +470,7 @@ def cpu_leg(args, eng, run, serial, seq_for, rot_for, reset_params, strat_sizes,
         "value": S / (t_sgd + t_sse), "unit": "rating-updates/s", "cores": 1, "kind": "port",
         "sample": (f"{what} of the same workload: FP64 sequential SGD sweep ({t_sgd:.1f}s) "
                    f"+ RMSE pass ({t_sse:.1f}s), oracle/mf_oracle.c, one thread"),
-        "sgd_only": S / t_sgd, **host,
+        "sgd_only": S / t_sgd, "affinity": core, **host,
     }
     parity = {
         "what": (f"{what} from the same initial state: (a) GPU FP32 strata vs CPU oracle "
@@ -478,6 +508,112 @@ def cpu_leg(args, eng, run, serial, seq_for, rot_for, reset_params, strat_sizes,
     return cpu_baseline, parity
 
 
+DRAW_SEED = 12345
+
+
+def strata_seq(ep: int, nb: int) -> np.ndarray:
+    """Stratum (colour) order of bench epoch ``ep``."""
+    return np.random.RandomState((DRAW_SEED * 1000003 + ep) & 0x7FFFFFFF).permutation(
+        nb).astype(np.int32)
+
+
+def strata_rot(ep: int) -> int:
+    """Step-rotation seed of bench epoch ``ep`` (rotate: the epoch's draw)."""
+    return (DRAW_SEED * 7919 + ep * 104729) & 0x7FFFFFFF
+
+
+def multi_checks(args, eng, rotate, world, rank, dev, u, i, r, nu, ni, k, kernel, mu, P0, Q0,
+                 n_ep, rmse) -> dict:
+    """N > 1, after the timed epochs (untimed): is the multi-GPU result
+    right?  Every rank takes part in the collectives; rank 0 also re-runs the
+    work on its own GPU.
+
+    replicas     a 64-bit fingerprint of each rank's [Q | b_i] replica
+                 (mf_fingerprint): all ranks must agree bit for bit;
+    replay       rotate: rank 0 runs the same N-rank rotation order on ONE GPU
+                 (distributed.RotationReplay: the same shards, item ranges,
+                 plans and draws, sub-blocks one after another) for the same
+                 epochs from the same start, and compares P, Q, b_u, b_i and
+                 the per-epoch RMSE with the N-GPU result (expected: bit-equal
+                 parameters -- the order is a sequential one, fixed by the plans
+                 and draws);
+    n1           rank 0 trains the same data from the same start for the same
+                 epochs with the single-GPU default (one strata plan over all
+                 ratings) and reports the RMSE gap (north star: RMSE matching
+                 the CPU reference to 1e-5; the N=1 run is pinned to the CPU
+                 oracle by the N=1 bench line's parity)."""
+    import torch
+    import torch.distributed as dist
+
+    from matrix_factorization import _lib
+    from matrix_factorization.distributed import RotationReplay, _gather_rows, shard_users
+    from matrix_factorization.engine import SGDEngine
+
+    t0 = time.time()
+    Qh = eng.Q.detach().cpu().numpy()
+    bih = eng.bi.detach().cpu().numpy()
+    lib = _lib.load()
+    fp = [int(lib.mf_fingerprint(np.ascontiguousarray(a).ctypes.data, a.nbytes))
+          for a in (Qh, bih)]
+    mine = torch.tensor([fp[0] & 0x7FFFFFFFFFFFFFFF, fp[1] & 0x7FFFFFFFFFFFFFFF],
+                        dtype=torch.int64, device=dev if args.backend == "nccl" else "cpu")
+    allfp = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allfp, mine)
+    allfp = [tuple(int(x) for x in t.cpu()) for t in allfp]
+    bounds = shard_users(u, nu, world)
+    Pg = _gather_rows(eng.P, bounds)
+    bug = _gather_rows(eng.bu.reshape(-1, 1), bounds).reshape(-1)
+    out = {"exchange": "rotate" if rotate else "delta",
+           "replica_fingerprints": [f"{a:016x}:{b:016x}" for a, b in allfp],
+           "replicas_agree": all(f == allfp[0] for f in allfp)}
+    if rank == 0 and not args.no_check:
+        hyp = dict(gamma=1.0 / k, min_rating=1.0, max_rating=5.0, global_mean=mu)
+        if rotate:
+            log("check: one-GPU replay of the N-rank rotation order")
+            rp = RotationReplay(u, i, r, nu, ni, world, k, kernel, args.dtype, dev,
+                                n_blocks=args.blocks, waves=args.waves, **hyp)
+            rp.load(P0, Q0, np.zeros(nu), np.zeros(ni))
+            sse = []
+            for ep in range(n_ep):
+                rp.epoch(strata_rot(ep), args.lr, args.reg)
+                sse.append(rp.sse(ep))
+            Pr, Qr, bur, bir = rp.params()
+            rm_r = [float(np.sqrt(x / len(u))) for x in sse]
+            d = {"dP": float(np.max(np.abs(Pr - Pg))),
+                 "dQ": float(np.max(np.abs(Qr - Qh.astype(np.float64)))),
+                 "dbu": float(np.max(np.abs(bur - bug))),
+                 "dbi": float(np.max(np.abs(bir - bih.astype(np.float64))))}
+            out["replay"] = {
+                "what": ("rank 0 ran the same N-rank rotation order on one GPU (RotationReplay) "
+                         f"for the same {n_ep} epochs from the same start"),
+                "max_abs_diff": d, "bit_equal": all(v == 0.0 for v in d.values()),
+                "max_abs_rmse_diff": float(np.max(np.abs(np.asarray(rm_r) - np.asarray(rmse)))),
+                "rmse_replay_final": rm_r[-1]}
+            del rp
+            torch.cuda.empty_cache()
+        log("check: N=1 leg (single-GPU default schedule, same data, start and epochs)")
+        e1 = SGDEngine(u, i, r, nu, ni, k, kernel, args.dtype, dev, **hyp)
+        e1.load_params(P=P0, Q=Q0, bu=np.zeros(nu), bi=np.zeros(ni))
+        plan1 = e1.prepare_strata()
+        for ep in range(n_ep):
+            e1.epoch_strata(strata_seq(ep, plan1.B), strata_rot(ep), args.lr, args.reg)
+            e1.sse_async(ep)
+        rm1 = e1.rmse_values(n_ep)
+        del e1
+        torch.cuda.empty_cache()
+        out["n1"] = {"what": (f"rank 0: the same {n_ep} epochs on one GPU with the single-GPU "
+                              "default schedule (the N=1 bench line's)"),
+                     "rmse_n1_final": rm1[-1], "rmse_final": rmse[-1],
+                     "rmse_gap_vs_n1": rmse[-1] - rm1[-1],
+                     "rmse_per_epoch_n1": rm1}
+        out["check_s"] = time.time() - t0
+        log(f"checks: replicas agree {out['replicas_agree']}, "
+            + (f"replay bit-equal {out['replay']['bit_equal']}, " if rotate else "")
+            + f"RMSE gap vs N=1 {out['n1']['rmse_gap_vs_n1']:+.3e}")
+    dist.barrier()
+    return out
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -503,9 +639,17 @@ def main() -> int:
     ap.add_argument("--schedule", default="strata", choices=["strata", "colored"],
                     help="strata: B x B blocks, item slabs in LDS (mf_strata.hpp); "
                          "colored: one launch per edge colour (mf_rows.hpp)")
+    ap.add_argument("--exchange", default="rotate", choices=["rotate", "delta"],
+                    help="N > 1 (strata): rotate = item ranges passed round the ring "
+                         "between N sub-epochs (exact: a sequential order, DESIGN.md 6); "
+                         "delta = item deltas all-reduced once per epoch, applied damped")
     ap.add_argument("--delta-scale", type=float, default=None,
-                    help="N > 1: weight of the all-reduced item deltas (default 1/N, "
-                         "model averaging; 1.0 = plain gradient sum)")
+                    help="N > 1, --exchange delta: weight of the all-reduced item deltas "
+                         "(default min(1/2, 2/N), distributed.default_delta_scale; "
+                         "1.0 = plain gradient sum)")
+    ap.add_argument("--no-check", action="store_true",
+                    help="N > 1: skip the post-timing checks (replica checksums on every "
+                         "rank, rank 0's one-GPU replay of the same order, the N=1 RMSE leg)")
     ap.add_argument("--rmse-overlap", action="store_true",
                     help="one GPU: run each epoch's RMSE pass on a side stream from a "
                          "parameter snapshot, beside the next epoch's sweep")
@@ -518,8 +662,9 @@ def main() -> int:
     import torch.distributed as dist
 
     from matrix_factorization import _lib
-    from matrix_factorization.distributed import (ReplicaExchange, global_rmse,
-                                                  local_shard, shard_users)
+    from matrix_factorization.distributed import (ReplicaExchange, RotationExchange,
+                                                  any_rank_failed, global_rmse, item_ranges,
+                                                  local_shard, rotation_epoch, shard_users)
     from matrix_factorization.engine import SGDEngine, strata_slots
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -570,13 +715,18 @@ def main() -> int:
                     gamma=1.0 / k, min_rating=1.0, max_rating=5.0, global_mean=mu)
     t0 = time.time()
     strata = args.schedule == "strata"
+    rotate = world > 1 and strata and args.exchange == "rotate"
+    ilo = item_ranges(i, ni, world) if rotate else None
     if strata:
-        plan = eng.prepare_strata(n_blocks=args.blocks, waves=args.waves)
+        plan = eng.prepare_strata(n_blocks=args.blocks, waves=args.waves, item_bounds=ilo)
         nb = plan.B
         n_phases = len(getattr(plan, "phases", [plan]))   # item phases (PhasedStrata)
         strat_sizes = plan.stratum_sizes()           # ratings per stratum (launch)
         fill = n_local / max(plan.n_positions, 1)
-        sched_desc = ((f"strata ({n_phases} item phases x B={nb} strata, " if n_phases > 1
+        sched_desc = ((f"strata rotation ({n_phases} item ranges passed round the ring: "
+                       f"{n_phases} sub-epochs x B={nb} strata on this rank's sub-block, "
+                       if rotate else
+                       f"strata ({n_phases} item phases x B={nb} strata, " if n_phases > 1
                        else f"strata (B={nb}: {nb} launches/epoch, ")
                       + "item slabs in LDS, "
                       f"{plan.NS} user-owned slots "
@@ -592,7 +742,9 @@ def main() -> int:
         sched_desc = f"colored ({nb} conflict-free batches/epoch on rank 0)"
     t_sched = time.time() - t0
     log(f"rank {rank}: {n_local} local ratings, {sched_desc}, scheduled in {t_sched:.1f}s")
-    exch = ReplicaExchange(eng, scale=args.delta_scale) if world > 1 else None
+    exch = (ReplicaExchange(eng, scale=args.delta_scale) if world > 1 and not rotate
+            else None)
+    rot = RotationExchange(eng, ilo) if rotate else None
 
     def reset_params():
         eng.load_params(P=P_local, bu=np.zeros(n_users_local))
@@ -601,17 +753,21 @@ def main() -> int:
         else:
             eng.load_params(Q=Q0, bi=np.zeros(ni))
 
-    seed = 12345
-
     def seq_for(ep):
-        return np.random.RandomState((seed * 1000003 + ep) & 0x7FFFFFFF).permutation(nb).astype(np.int32)
+        return strata_seq(ep, nb)
 
-    def rot_for(ep):          # colour-rotation seed of a strata epoch
-        return (seed * 7919 + ep * 104729) & 0x7FFFFFFF
+    def rot_for(ep):          # colour-rotation seed of a strata epoch (rotate: the epoch draw)
+        return strata_rot(ep)
 
-    def run(ep, seq, timing=False):
+    def run(ep, seq, timing=False, events=None):
         """The local sweep of epoch ep (N > 1, strata: delta-out form -- the
-        replica stays put and the item update lands in exch.delta)."""
+        replica stays put and the item update lands in exch.delta; rotate:
+        the whole rotation epoch, hand-offs and final all-gather included)."""
+        if rotate:
+            launches = [] if timing else None
+            rotation_epoch(eng, rot, rot_for(ep), args.lr, args.reg, events=events,
+                           launches=launches)
+            return (None, sum(launches)) if timing else None
         if strata:
             delta = None if exch is None else (exch.dq, exch.dbi)
             return eng.epoch_strata(seq, rot_for(ep), args.lr, args.reg, timing=timing,
@@ -657,16 +813,23 @@ def main() -> int:
     # 1.146 ms) -- DESIGN.md section 5
     overlap = world == 1 and args.rmse_overlap
 
+    rot_events = []   # rotate: per timed epoch, the (kind, start, end) events of its parts
+
     def epoch(ep, timed):
         # hipEvents on the stream the kernels run on (torch's current stream,
         # which the engine launches on): one pair around the epoch's SGD
         # launches, one more after the RMSE pass -- no host sync in the loop.
+        # rotate: every sub-epoch and hand-off bracketed too (rot_events).
         seq = seq_for(ep)
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if (timed and phase) else None
         begin()
         if ev:
             ev[0].record()
-        run(ep, seq)
+        if rotate and ev:
+            rot_events.append([])
+            run(ep, seq, events=rot_events[-1])
+        else:
+            run(ep, seq)
         if ev:
             ev[1].record()
         end()
@@ -692,6 +855,9 @@ def main() -> int:
             if persistent:           # one persistent launch per epoch (per item phase)
                 sched_desc = sched_desc.replace(
                     f"B={nb}: {nb} launches/epoch", f"B={nb} strata in 1 persistent launch/epoch")
+                if rotate:
+                    sched_desc = sched_desc.replace("strata on this rank's sub-block",
+                                                    "strata in 1 persistent launch per sub-epoch")
             launches_per_epoch = n_launch
         else:
             epoch(ep, False)
@@ -712,10 +878,15 @@ def main() -> int:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    if strata:
-        eng.check_strata()          # raises if a persistent sweep gave up waiting
+    if strata and any_rank_failed(eng):  # every rank raises together: nobody left waiting
+        raise SystemExit("a persistent strata sweep gave up waiting (workgroups not "
+                         "co-resident): the timed epochs are invalid")
     n_ep = args.warmup + args.steps
     rmse = global_rmse(eng, n_ep, nnz)
+    multi = None
+    if world > 1:
+        multi = multi_checks(args, eng, rotate, world, rank, dev, u, i, r, nu, ni, k, kernel, mu,
+                             P0, Q0, n_ep, rmse)
 
     if rank == 0:
         value = nnz * args.steps / elapsed
@@ -746,16 +917,25 @@ def main() -> int:
             sgd_s = sum(e[0].elapsed_time(e[1]) for e in events) / 1e3
             exch_s = sum(e[1].elapsed_time(e[2]) for e in events) / 1e3
             sse_s = sum(e[2].elapsed_time(e[3]) for e in events) / 1e3
+            if rotate:      # split the rotation epoch into its sweeps and hand-offs
+                part = {"sgd": 0.0, "pass": 0.0, "gather": 0.0}
+                for evs in rot_events:
+                    for kind, a, b in evs:
+                        part[kind] += a.elapsed_time(b) / 1e3
+                sgd_s = part["sgd"]
+                exch_s = part["pass"] + part["gather"]
             launches = launches_per_epoch * len(events)
             alg = alg_epoch * len(events)                           # algorithmic bytes
             achieved = alg / sgd_s / 1e9
+            kname = (("k_sgd_strata_epoch" if persistent else "k_sgd_strata") if strata
+                     else "k_sgd_batch")
             traffic = traffic_from_profiles(args.workload, world, args.schedule
-                                            + ("_persistent" if persistent else ""))
+                                            + ("_persistent" if persistent else ""),
+                                            args.dtype, kname)
             roofline = {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "kernel": ("k_sgd_strata_epoch" if persistent else "k_sgd_strata") if strata
-                          else "k_sgd_batch", "launches": launches,
+                "kernel": kname, "launches": launches,
                 "avg_launch_us": sgd_s / launches * 1e6,
                 "avg_launch_note": "SGD phase time / launches (hipEvents around each "
                                    "epoch's SGD launches on the launch stream)",
@@ -779,6 +959,9 @@ def main() -> int:
                                              "the parameters, beside the next epoch's sweep")
             if world > 1:
                 phases["exchange_ms_per_epoch"] = exch_s / len(events) * 1e3
+                if rotate:
+                    phases["ring_pass_ms_per_epoch"] = part["pass"] / len(events) * 1e3
+                    phases["gather_ms_per_epoch"] = part["gather"] / len(events) * 1e3
         out = {
             "metric": METRIC, "value": value, "unit": "rating-updates/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -790,13 +973,14 @@ def main() -> int:
                        "n_factors": k, "kernel": kernel, "lr": args.lr, "reg": args.reg,
                        "schedule": sched_desc,
                        "parallelism": f"user-sharded dp{world}" if world > 1 else "single GPU",
+                       "exchange": (None if world == 1 else "rotate" if rotate else "delta"),
                        "item_delta_scale": None if exch is None else exch.scale,
                        "step": "one epoch: SGD sweep + training-RMSE pass" +
                                (" (epoch e's RMSE overlapped with epoch e+1's sweep)"
                                 if overlap else "")},
             "final_rmse": rmse[-1], "rmse_per_epoch": rmse,
             "roofline": roofline, "phases": phases,
-            "cpu_baseline": cpu_baseline, "parity": parity,
+            "cpu_baseline": cpu_baseline, "parity": parity, "multi_gpu": multi,
             "schedule_build_s": t_sched,
         }
         print(json.dumps(out), flush=True)

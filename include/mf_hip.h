@@ -177,7 +177,11 @@ int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_ids,
  * are left at their values before the call, and item_delta (DEVICE, n_items
  * x n_factors) / item_bias_delta (DEVICE, n_items; unused by rbf) receive
  * the local update (value after the epoch - value before).  The caller
- * all-reduces the deltas and adds the sum (mf_replica_delta, MF_DELTA_APPLY).
+ * all-reduces the deltas and adds them damped with mf_replica_apply, scale =
+ * min(1/2, 2/world) (distributed.default_delta_scale: the plain sum diverges
+ * at N >= 4 on C3).  This is the "delta" exchange; the default "rotate"
+ * exchange needs no delta form (ranks pass item ranges instead, each applied
+ * in place by mf_sgd_epoch_strata on its rows of Q / b_i).
  * The persistent kernel writes the delta where it would write the slab back;
  * the per-stratum fallback keeps the start values in the delta buffers and
  * swaps at the end.  User rows and biases are updated in place as usual.
@@ -209,6 +213,11 @@ int32_t mf_strata_lds_limit(void);
  * (100 MHz) per (position t, workgroup w) at [(t*B + w)*4 + q]: q = 0 wait
  * start, 1 wait end, 2 block end, 3 signal.  NULL turns it off (default). */
 int mf_strata_set_probe(int64_t* probe);
+/* Test hook: the next n_launches persistent strata launches of this process
+ * start with their error word set, as if a neighbour wait had timed out, so
+ * callers can exercise their recovery (KernelMF.fit / distributed.fit_sharded
+ * replay the epochs as per-stratum launches).  0 turns it off. */
+int mf_strata_inject_fail(int32_t n_launches);
 /* Rating slots per step of the strata kernel for (n_factors, dtype); -1 on
  * invalid arguments. */
 int32_t mf_strata_slots(int32_t n_factors, int32_t dtype);
@@ -264,8 +273,10 @@ int mf_predict(const int32_t* user_ids, const int32_t* item_ids,
  * prediction of every item, as recommend() scores them,
  * recommender_base.py:245-260).  Exclusions (recommend's items_known,
  * :245-250) as a DEVICE CSR list, both nullable: the items
- * exclude_items[exclude_ptr[q] .. exclude_ptr[q+1]) (int32, any order; ids
- * outside [0, n_items) ignored) are skipped for query q.  Ties are broken by
+ * exclude_items[exclude_ptr[q] .. exclude_ptr[q+1]) (int32, each user's list
+ * SORTED ASCENDING -- the kernels binary-search it; ids outside [0, n_items)
+ * ignored) are skipped for query q.  An unsorted list makes the result
+ * undefined (items may come back although listed).  Ties are broken by
  * the lower item id (the order a stable sort_values gives; the reference's
  * default quicksort leaves tie order unspecified, :259).  out_items (int32) /
  * out_scores (dtype): device, n_query * amount.  Rows with fewer than
@@ -295,6 +306,7 @@ int mf_topk(const int32_t* query_users, int32_t n_query, double global_mean,
  * a candidate band outgrew its list (masses of near-equal scores): the
  * results are then not guaranteed and the caller re-runs mf_topk.  Items
  * whose score is NaN are never candidates here (mf_topk ranks them last).
+ * Exclusion lists as for mf_topk: each user's list sorted ascending.
  * workspace: device, >= mf_topk_mm_workspace_bytes(n_query, n_items).
  */
 int32_t mf_topk_mm_supported(int32_t n_factors, int32_t kernel, int32_t dtype,
@@ -396,7 +408,8 @@ int mf_als_sweep_probe(const int64_t* entity_ptr, const int32_t* other_ids,
 
 /*
  * Element-wise helper around the per-epoch all-reduce of the replicated item
- * parameters (user-sharded data parallelism; no
+ * parameters (user-sharded data parallelism, "delta" exchange, DESIGN.md
+ * section 6; no
  * counterpart in the single-process reference):
  *   mode 0 (MF_DELTA_TAKE):  cur[j] = cur[j] - base[j]   (local update delta)
  *   mode 1 (MF_DELTA_APPLY): cur[j] = cur[j] + base[j]   (base + summed delta)
@@ -406,10 +419,11 @@ enum { MF_DELTA_TAKE = 0, MF_DELTA_APPLY = 1 };
 int mf_replica_delta(void* cur, const void* base, int64_t n, int32_t dtype,
                      int32_t mode, void* stream);
 /* cur[j] = cur[j] + scale * delta[j] (device, n values of dtype): applies
- * the all-reduced item deltas; scale = 1 / world (model averaging) is the
- * default of the sharded epoch -- the plain sum (scale 1) overshoots once
- * each rank's local epoch moves an item most of the way to its local optimum
- * (measured at C3: N = 4 and 8 diverge). */
+ * the all-reduced item deltas; scale = min(1/2, 2/world) is the default of
+ * the delta exchange (distributed.default_delta_scale) -- the plain sum
+ * (scale 1) overshoots once each rank's local epoch moves an item most of the
+ * way to its local optimum (measured at C3: N = 4 and 8 diverge), plain
+ * averaging (1/world) under-steps. */
 int mf_replica_apply(void* cur, const void* delta, int64_t n, int32_t dtype, double scale,
                      void* stream);
 

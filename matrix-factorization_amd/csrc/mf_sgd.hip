@@ -6,6 +6,7 @@
 // Compiled with -ffp-contract=off: every scalar expression rounds like the
 // reference's FP64 evaluation of the same expression; only the k-long sums
 // follow a fixed DPP order instead of BLAS ddot's.
+#include <atomic>
 #include <algorithm>
 #include <type_traits>
 #include <vector>
@@ -255,10 +256,26 @@ extern "C" int32_t mf_strata_lds_limit(void) { return kLdsLimit; }
 namespace mf {
 static int64_t* g_strata_probe = nullptr;
 int64_t* strata_probe_ptr() { return g_strata_probe; }
+static std::atomic<int32_t> g_strata_inject{0};
+bool strata_inject_fail() {
+    int32_t v = g_strata_inject.load();
+    while (v > 0)
+        if (g_strata_inject.compare_exchange_weak(v, v - 1)) return true;
+    return false;
+}
 }  // namespace mf
 
 extern "C" int mf_strata_set_probe(int64_t* probe) {
     mf::g_strata_probe = probe;
+    return MF_OK;
+}
+
+extern "C" int mf_strata_inject_fail(int32_t n_launches) {
+    if (n_launches < 0) {
+        set_error("mf_strata_inject_fail: n_launches < 0");
+        return MF_ERR_INVALID;
+    }
+    mf::g_strata_inject.store(n_launches);
     return MF_OK;
 }
 

@@ -640,6 +640,14 @@ inline size_t strata_ws_bytes(int32_t B, int32_t n_seq) {
     return sizeof(int32_t) * ((size_t)B + 1 + (size_t)n_seq);
 }
 
+// Fault-injection hook for the callers' recovery paths (tests only,
+// mf_strata_inject_fail): the next n persistent launches of this process
+// start with the error word set, as if a neighbour wait had timed out
+// (workgroups that poll see it and leave; the word stays set, so the caller
+// must detect the failure and recover exactly as after a real timeout).
+// True (and one fewer left) if this launch is one of them.
+bool strata_inject_fail();
+
 // Can all B workgroups of `kfn` be resident at once (the persistent kernel's
 // waits need it)?
 inline bool strata_coresident(const void* kfn, int B, size_t lds, int threads) {
@@ -769,6 +777,9 @@ struct StrataRun {
                 const int32_t* dseq = err + 1;
                 int32_t nseq = p.n_seq;
                 MF_HIP_CHECK(hipMemsetAsync(done, 0, sizeof(int32_t) * (size_t)p.B, p.stream));
+                if (strata_inject_fail())
+                    MF_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(err), 1, 1,
+                                                   p.stream));
                 MF_HIP_CHECK(hipMemcpyAsync(err + 1, p.seq, sizeof(int32_t) * (size_t)p.n_seq,
                                             hipMemcpyHostToDevice, p.stream));
                 if (p.flags & MF_FLAG_NO_COOP) {

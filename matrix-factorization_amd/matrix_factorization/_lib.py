@@ -110,6 +110,7 @@ SIGNATURES = {
     "mf_strata_plan_fetch": (ctypes.c_int, [_P, _P, _P]),
     "mf_strata_plan_free": (None, [_P]),
     "mf_strata_set_probe": (ctypes.c_int, [_P]),
+    "mf_strata_inject_fail": (ctypes.c_int, [_I32]),
     "mf_legacy_shuffle": (ctypes.c_int, [_P, _P, _P, _I64]),
     "mf_pairs_duplicated": (ctypes.c_int, [_P, _P, _I64, _P]),
     "mf_factorize": (ctypes.c_int, [_P, _I64, _P, _P, _P]),

@@ -2,10 +2,27 @@
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL on ROCm; "gloo"
 for CPU rehearsal of the control flow).  The reference is single-process; this
-is the build's multi-GPU extension of the same epoch:
+is the build's multi-GPU extension of the same epoch.
+Users are split into contiguous internal-id ranges balanced by rating count;
+a rank owns its users' rows of P and b_u and all of their ratings.  Two ways
+to keep the item side consistent:
 
-* users are split into contiguous internal-id ranges balanced by rating count;
-  a rank owns its users' rows of P and b_u and all of their ratings;
+``exchange="rotate"`` (the default; exact).  Items are cut into N contiguous
+ranges too, so the ratings form an N x N grid of sub-blocks (user range r x
+item range c).  An epoch is N sub-epochs; in sub-epoch s rank r sweeps its
+sub-block with item range c = (r + off + s) mod N -- the N sub-blocks of a
+sub-epoch share no user and no item -- in place on its rows of Q / b_i (one
+persistent strata launch of that item range's plan, engine.epoch_phase), then
+hands the range to rank r - 1 and receives range c + 1 from rank r + 1 (ring
+send / recv of n_items / N rows over xGMI).  After the last sub-epoch every
+range is final on exactly one rank and one all-gather gives every rank the
+whole replica (the training-RMSE pass reads it).  Every rating is applied
+with the current user AND item rows: the epoch is the sequential sweep of a
+stated serial order (sub-epoch by sub-epoch, ranks in any order), the
+strata schedule at GPU granularity -- ``RotationReplay`` runs the same order
+on one GPU bit for bit, and the oracle replays it (tests).
+
+``exchange="delta"`` (damped; item updates one epoch late):
 * Q and b_i are replicated and kept in ONE flat buffer [Q | b_i], so the
   exchange is a single collective;
 * per epoch (strata): the local persistent sweep runs in delta-out form
@@ -19,9 +36,9 @@ is the build's multi-GPU extension of the same epoch:
 * the training SSE of every epoch stays on the device and is summed across
   ranks once (or per epoch when the caller prints it).
 
-Item updates are thereby delayed by up to one epoch relative to the
-sequential sweep and combined with a damped sum (user updates are exact):
-RMSE is reported next to the 1-GPU run, not claimed identical.  The plain
+In delta mode item updates are thereby delayed by up to one epoch relative
+to the sequential sweep and combined with a damped sum (user updates are
+exact): RMSE is reported next to the 1-GPU run, not claimed identical.  The plain
 sum of the deltas (scale 1, "all-reduce of the gradients") is available but
 is not the default: each rank's local epoch moves an item much of the way
 toward its local optimum, so N summed moves overshoot and C3 diverges at
@@ -33,6 +50,7 @@ distributed=True).fit on every rank with the same data and RNG state).
 
 from __future__ import annotations
 
+import warnings
 from typing import Optional, Tuple
 
 import numpy as np
@@ -40,7 +58,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .engine import SGDEngine, _tp
+from .engine import SGDEngine, _tp, balanced_bounds
 
 
 def world_info(group=None) -> Tuple[int, int]:
@@ -138,10 +156,16 @@ class ReplicaExchange:
 
     # ---- strata: delta-out sweep, all-reduce, apply
     def strata_epoch(self, seq, seed, lr, reg, update_user=True, update_item=True,
-                     timing=False):
+                     timing=False, persistent=None, exchange=True):
+        """Delta-out sweep, then (``exchange``) all-reduce + apply.  With the
+        item side frozen there is nothing to exchange: the sweep runs in place."""
+        if not update_item:
+            return self.e.epoch_strata(seq, seed, lr, reg, update_user, False, timing=timing,
+                                       persistent=persistent)
         ms = self.e.epoch_strata(seq, seed, lr, reg, update_user, update_item, timing=timing,
-                                 delta=(self.dq, self.dbi))
-        self.exchange()
+                                 delta=(self.dq, self.dbi), persistent=persistent)
+        if exchange:
+            self.exchange()
         return ms
 
     def exchange(self) -> None:
@@ -167,6 +191,240 @@ class ReplicaExchange:
         self.e.bi = self.flat[n * k:]
         self.dq = self.delta[: n * k].view(n, k)
         self.dbi = self.delta[n * k:]
+
+
+# ------------------------------------------------------------------ rotate
+EXCHANGES = ("rotate", "delta")
+
+
+def item_ranges(item_ids: np.ndarray, n_items: int, world: int) -> np.ndarray:
+    """``world`` contiguous item-id ranges (world + 1 int64 bounds) with about
+    equal rating counts: the item ranges the rotation schedule passes round
+    the ring.  Ranges stay non-empty while n_items >= world."""
+    b = balanced_bounds(np.asarray(item_ids, np.int32), n_items, world).astype(np.int64)
+    if n_items >= world:                    # no empty range (a degenerate rating skew)
+        for c in range(1, world):
+            b[c] = min(max(b[c], b[c - 1] + 1), n_items - (world - c))
+    return b
+
+
+def rotation_offset(draw: int, world: int) -> int:
+    """Item range of rank 0 in sub-epoch 0 of the epoch with this draw."""
+    return int(draw) % world
+
+
+def rotation_range(rank: int, off: int, s: int, world: int) -> int:
+    """Item range rank ``rank`` sweeps in sub-epoch ``s``."""
+    return (rank + off + s) % world
+
+
+def rotation_draws(draw: int, rank: int, c: int, nb: int):
+    """Stratum order and step rotation of rank ``rank``'s sub-block with item
+    range ``c`` in the epoch with ``draw`` (reproducible per sub-block)."""
+    rs = np.random.RandomState([int(draw) & 0x7FFFFFFF, rank, c])
+    return rs.permutation(nb).astype(np.int32), int(rs.randint(0, 2**31 - 1))
+
+
+class RotationExchange:
+    """The ring hand-off of item ranges (``exchange="rotate"``).
+
+    The engine's Q / b_i hold the full item side; at any moment only the
+    range this rank holds is current there.  ``pass_range`` sends range
+    ``c_send`` to rank - 1 and receives ``c_recv`` from rank + 1 (batched
+    point-to-point: one RCCL group, two xGMI transfers per rank);
+    ``gather`` all-gathers every rank's final range at the end of an epoch.
+    With gloo and device tensors (one-GPU rehearsal) the transfers are
+    staged through host memory."""
+
+    def __init__(self, engine: SGDEngine, ilo: np.ndarray, group=None):
+        self.e, self.group = engine, group
+        self.ilo = np.asarray(ilo, np.int64)
+        self.world, self.rank = world_info(group)
+        if len(self.ilo) != self.world + 1:
+            raise ValueError("item ranges must be one per rank")
+        dev = getattr(engine, "dev", torch.device("cpu"))
+        self.stage = (self.world > 1 and dist.get_backend(group) == "gloo"
+                      and torch.device(dev).type == "cuda")
+        self.rows = int(np.diff(self.ilo).max()) if self.world else 0
+        self._gbuf = None
+
+    def _range(self, c: int):
+        lo, hi = int(self.ilo[c]), int(self.ilo[c + 1])
+        return self.e.Q[lo:hi], self.e.bi[lo:hi]
+
+    def pass_range(self, c_send: int, c_recv: int) -> None:
+        """Send range c_send to rank - 1, receive range c_recv from rank + 1."""
+        if self.world == 1:
+            return
+        to, frm = (self.rank - 1) % self.world, (self.rank + 1) % self.world
+        qs, bs = self._range(c_send)
+        qr, br = self._range(c_recv)
+        if self.stage:
+            snd = [qs.cpu(), bs.cpu()]
+            rcv = [torch.empty_like(qr, device="cpu"), torch.empty_like(br, device="cpu")]
+        else:
+            snd, rcv = [qs, bs], [qr, br]
+        ops = ([dist.P2POp(dist.isend, t, to, self.group) for t in snd]
+               + [dist.P2POp(dist.irecv, t, frm, self.group) for t in rcv])
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        if self.stage:
+            qr.copy_(rcv[0])
+            br.copy_(rcv[1])
+
+    def gather(self, c_final: list) -> None:
+        """Every rank's final range (rank r holds c_final[r]) to every rank."""
+        if self.world == 1:
+            return
+        e, k, m = self.e, self.e.k, self.rows
+        dev = torch.device("cpu") if self.stage else e.Q.device
+        if self._gbuf is None:
+            self._gbuf = (torch.zeros(m * (k + 1), dtype=e.Q.dtype, device=dev),
+                          torch.empty(self.world * m * (k + 1), dtype=e.Q.dtype, device=dev))
+        mine, out = self._gbuf
+        q, b = self._range(c_final[self.rank])
+        n = q.shape[0]
+        mine[: n * k].copy_(q.reshape(-1))
+        mine[m * k: m * k + n].copy_(b)
+        if dist.get_backend(self.group) == "gloo":
+            dist.all_gather(list(out.view(self.world, -1).unbind(0)), mine, group=self.group)
+        else:
+            dist.all_gather_into_tensor(out, mine, group=self.group)
+        parts = out.view(self.world, m * (k + 1))
+        for r in range(self.world):
+            if r == self.rank:
+                continue
+            q, b = self._range(c_final[r])
+            n = q.shape[0]
+            q.copy_(parts[r, : n * k].view(n, k))
+            b.copy_(parts[r, m * k: m * k + n])
+
+
+def rotation_epoch(engine: SGDEngine, rot: RotationExchange, draw: int, lr: float, reg: float,
+                   update_user: bool = True, update_item: bool = True, events=None,
+                   persistent: Optional[bool] = None, launches: Optional[list] = None) -> None:
+    """One epoch of the rotation schedule on this rank (module docstring):
+    N sub-epochs (engine.epoch_phase on the range held), N - 1 ring hand-offs,
+    one all-gather.  ``events``: a list that receives (kind, start, end)
+    timing events ("sgd" / "pass" / "gather") recorded on the launch stream.
+    ``launches``: a list that receives each sub-epoch's kernel launch count
+    (1 = persistent; synchronises after every sub-epoch)."""
+    world, rank = rot.world, rot.rank
+    nb = engine.strata.B
+    off = rotation_offset(draw, world)
+
+    def mark(kind, fn):
+        if events is None:
+            return fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = fn()
+        e1.record()
+        events.append((kind, e0, e1))
+        return out
+
+    for s in range(world):
+        c = rotation_range(rank, off, s, world)
+        seq, seed = rotation_draws(draw, rank, c, nb)
+        out = mark("sgd", lambda: engine.epoch_phase(c, seq, seed, lr, reg, update_user,
+                                                     update_item, persistent=persistent,
+                                                     timing=launches is not None))
+        if launches is not None:
+            launches.append(int(out[1]))
+        if s + 1 < world:
+            mark("pass", lambda: rot.pass_range(c, rotation_range(rank, off, s + 1, world)))
+    mark("gather", lambda: rot.gather([rotation_range(r, off, world - 1, world)
+                                       for r in range(world)]))
+
+
+class RotationReplay:
+    """The N-rank rotation schedule on ONE GPU (rehearsal and check).
+
+    One engine per virtual rank -- the same user shard, item ranges and plans
+    a real rank builds -- all pointing at one shared [Q, b_i]; sub-epoch s runs
+    every rank's sub-block (r, (r + off + s) mod N) one after another.  The
+    sub-blocks of a sub-epoch are disjoint in users and items, so this is bit
+    for bit what N GPUs compute (the kernel's arithmetic depends only on the
+    plan, the draws and the values), and each rank's sub-epoch time is
+    measured alone.  ``serial_order`` lists the epoch's sequential order for
+    the oracle."""
+
+    def __init__(self, u, i, r, n_users: int, n_items: int, world: int, n_factors: int,
+                 kernel: str, dtype: str, device, gamma: float = 0.0, min_rating: float = 0.0,
+                 max_rating: float = 5.0, global_mean: float = 0.0,
+                 n_blocks: Optional[int] = None, waves: Optional[int] = None, engine_cls=None):
+        make = SGDEngine if engine_cls is None else engine_cls
+        self.world = world
+        self.bounds = shard_users(u, n_users, world)
+        self.ilo = item_ranges(i, n_items, world)
+        self.n_items, self.n = n_items, len(u)
+        self.engines, self.gidx = [], []
+        for rank in range(world):
+            lo, hi = int(self.bounds[rank]), int(self.bounds[rank + 1])
+            m = (u >= lo) & (u < hi)
+            self.gidx.append(np.flatnonzero(m))
+            e = make(u[m] - lo, i[m], r[m], hi - lo, n_items, n_factors, kernel, dtype, device,
+                     gamma=gamma, min_rating=min_rating, max_rating=max_rating,
+                     global_mean=global_mean)
+            if waves is None:
+                e.prepare_strata(n_blocks=n_blocks, item_bounds=self.ilo)
+            else:
+                e.prepare_strata(n_blocks=n_blocks, waves=waves, item_bounds=self.ilo)
+            self.engines.append(e)
+        # one B for every rank (each rank's plans draw their strata from it)
+        self.B = [e.strata.B for e in self.engines]
+
+    def load(self, P0, Q0, bu0, bi0) -> None:
+        e0 = self.engines[0]
+        e0.load_params(Q=Q0, bi=bi0)
+        for rank, e in enumerate(self.engines):
+            lo, hi = int(self.bounds[rank]), int(self.bounds[rank + 1])
+            e.load_params(P=P0[lo:hi], bu=bu0[lo:hi])
+            e.Q, e.bi = e0.Q, e0.bi
+
+    def epoch(self, draw: int, lr: float, reg: float, update_user=True, update_item=True,
+              timing: bool = False, persistent: Optional[bool] = None):
+        """One rotation epoch; with ``timing`` the kernel ms of every
+        (sub-epoch, rank) as a world x world array."""
+        W = self.world
+        off = rotation_offset(draw, W)
+        ms = np.zeros((W, W))
+        for s in range(W):
+            for rank, e in enumerate(self.engines):
+                c = rotation_range(rank, off, s, W)
+                seq, seed = rotation_draws(draw, rank, c, e.strata.B)
+                t = e.epoch_phase(c, seq, seed, lr, reg, update_user, update_item,
+                                  timing=timing, persistent=persistent)
+                if timing:
+                    ms[s, rank] = t[0]
+        return ms if timing else None
+
+    def serial_order(self, draw: int) -> np.ndarray:
+        """Global rating indices in the order one epoch applies them."""
+        W = self.world
+        off = rotation_offset(draw, W)
+        parts = []
+        for s in range(W):
+            for rank, e in enumerate(self.engines):
+                c = rotation_range(rank, off, s, W)
+                seq, seed = rotation_draws(draw, rank, c, e.strata.B)
+                parts.append(self.gidx[rank][e.strata.phase_order(c, seq, seed)])
+        return np.concatenate(parts).astype(np.int64)
+
+    def sse(self, slot: int) -> float:
+        tot = 0.0
+        for e in self.engines:
+            e.sse_async(slot)
+            tot += float(e.sse_values(slot + 1)[slot])
+        return tot
+
+    def params(self):
+        """(P, Q, b_u, b_i) float64 host arrays, users in global order."""
+        P = np.concatenate([e.P.cpu().numpy().astype(np.float64) for e in self.engines])
+        bu = np.concatenate([e.bu.cpu().numpy().astype(np.float64) for e in self.engines])
+        e0 = self.engines[0]
+        return (P, e0.Q.cpu().numpy().astype(np.float64), bu,
+                e0.bi.cpu().numpy().astype(np.float64))
 
 
 def epoch_draws(rs: np.random.RandomState, nb: int, strata: bool):
@@ -247,22 +505,51 @@ def _gather_rows(local: torch.Tensor, bounds: np.ndarray, group=None) -> np.ndar
                            for p, s in zip(parts, sizes)])
 
 
+def any_rank_failed(engine: SGDEngine, group=None) -> bool:
+    """True on every rank if a persistent strata sweep gave up waiting on ANY
+    rank since its error word was last cleared (synchronises; one MAX
+    all-reduce, so all ranks take the same branch and none is left waiting in
+    a collective)."""
+    bad = 1 if (engine.strata is not None and engine.strata_failed()) else 0
+    if not (dist.is_available() and dist.is_initialized()):
+        return bool(bad)
+    dev = (torch.device("cpu") if dist.get_backend(group) == "gloo"
+           else getattr(engine, "dev", torch.device("cpu")))
+    t = torch.tensor([bad], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return bool(int(t.item()))
+
+
 def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_items: int,
                 P0: np.ndarray, Q0: np.ndarray, bu0: np.ndarray, bi0: np.ndarray,
                 n_epochs: int, kernel: str, n_factors: int, dtype: str, device, gamma: float,
                 min_rating: float, max_rating: float, global_mean: float, lr: float,
                 reg: float, schedule: str, verbose: int = 0, update_user: bool = True,
-                update_item: bool = True, group=None):
+                update_item: bool = True, group=None, exchange: str = "rotate"):
     """KernelMF.fit's epochs in process-group mode (every rank calls it with
     the same ratings, initial parameters and NumPy RNG state).
 
     Each epoch draws ONE integer from NumPy's global RandomState on every
-    rank (the same value: same state) and derives the rank's stratum /
-    colour order from (that integer, rank).  Returns (P, Q, b_u, b_i,
-    train_rmse) as float64 host arrays, identical on every rank."""
+    rank (the same value: same state).  ``exchange="rotate"`` (strata, item
+    updates on): the rotation epoch (module docstring; the draw fixes the
+    ranges' order and each sub-block's strata); otherwise the rank's stratum /
+    colour order comes from (that integer, rank) and the item deltas are
+    all-reduced (``"delta"``; also ``update_item=False``, which needs no
+    exchange at all since the item side is frozen).
+
+    No host synchronisation per epoch: the persistent sweeps' error words are
+    sticky and checked on all ranks at once (any_rank_failed) where the host
+    waits anyway -- the verbose RMSE print or the end; if any rank's sweep gave
+    up waiting, every rank restores its start-of-fit snapshot and replays the
+    epochs so far with the same draws as per-stratum launches (same result).
+
+    Returns (P, Q, b_u, b_i, train_rmse, engine) with float64 host arrays,
+    identical on every rank."""
     if schedule not in ("strata", "colored"):
         raise ValueError("distributed fit needs schedule='strata' or 'colored' "
                          "(the exact schedule is one sequential order)")
+    if exchange not in EXCHANGES:
+        raise ValueError(f"exchange must be one of {EXCHANGES}, got {exchange!r}")
     world, rank = world_info(group)
     bounds = shard_users(u, n_users, world)
     lu, li, lr_ = local_shard(u, i, r, bounds, rank)
@@ -271,35 +558,79 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
                     gamma=gamma, min_rating=min_rating, max_rating=max_rating,
                     global_mean=global_mean)
     eng.load_params(P=P0[lo:hi], bu=bu0[lo:hi])
-    ex = ReplicaExchange(eng, group)
-    ex.bind(Q0, bi0)
     strata = schedule == "strata"
-    if strata:
-        eng.prepare_strata()
+    rotate = strata and exchange == "rotate" and update_item
+    ex = rot = None
+    if rotate:
+        eng.load_params(Q=Q0, bi=bi0)
+        ilo = item_ranges(i, n_items, world)
+        eng.prepare_strata(item_bounds=ilo)
+        rot = RotationExchange(eng, ilo, group)
         nb = eng.strata.B
     else:
-        eng.prepare_colored()
-        nb = len(eng.colored) - 1
+        ex = ReplicaExchange(eng, group)
+        ex.bind(Q0, bi0)
+        if strata:
+            eng.prepare_strata()
+            nb = eng.strata.B
+        else:
+            eng.prepare_colored()
+            nb = len(eng.colored) - 1
     n_total = len(u)
     rmse = []
+    draws = []
+    persistent = None
+    snap0 = None
+    if strata and eng.strata_persistent:
+        snap0 = (eng.snapshot_params(), None if ex is None else ex.flat.clone())
+
+    def run_epoch(epoch, draw, persistent_):
+        if rotate:
+            rotation_epoch(eng, rot, draw, lr, reg, update_user, update_item,
+                           persistent=persistent_)
+        else:
+            seq, sd = epoch_draws(np.random.RandomState([draw, rank]), nb, strata)
+            if strata:
+                ex.strata_epoch(seq, sd, lr, reg, update_user, update_item,
+                                persistent=persistent_, exchange=update_item)
+            else:
+                ex.begin_epoch()
+                eng.epoch_colored(seq, lr, reg, update_user, update_item)
+                ex.end_epoch()
+        eng.sse_async(epoch)
+
+    def replay(upto):
+        nonlocal persistent
+        warnings.warn(f"a persistent strata sweep could not complete within epochs 1-{upto} "
+                      "on some rank (workgroups not co-resident); every rank replayed them "
+                      "with the same draws as one launch per stratum", RuntimeWarning,
+                      stacklevel=3)
+        persistent = False
+        eng.restore_params(snap0[0])
+        if ex is not None:
+            ex.flat.copy_(snap0[1])
+        eng.clear_strata_error()
+        for ep in range(upto):
+            run_epoch(ep, draws[ep], False)
+
+    def check(upto):
+        if snap0 is not None and persistent is None and any_rank_failed(eng, group):
+            replay(upto)
+
     for epoch in range(n_epochs):
         draw = int(np.random.randint(0, 2**31 - 1))
-        seq, rot = epoch_draws(np.random.RandomState([draw, rank]), nb, strata)
-        if strata:
-            ex.strata_epoch(seq, rot, lr, reg, update_user, update_item)
-        else:
-            ex.begin_epoch()
-            eng.epoch_colored(seq, lr, reg, update_user, update_item)
-            ex.end_epoch()
-        eng.sse_async(epoch)
+        draws.append(draw)
+        run_epoch(epoch, draw, persistent)
         if verbose == 1:
+            check(epoch + 1)
             rm = global_rmse(eng, epoch + 1, n_total, group)[epoch]
             rmse.append(rm)
             if rank == 0:
                 print("Epoch ", epoch + 1, "/", n_epochs, " -  train_rmse:", rm)
-    if strata:
-        eng.check_strata()
+    check(n_epochs)
     if verbose != 1:
+        rmse = global_rmse(eng, n_epochs, n_total, group)
+    elif persistent is False:           # a replay re-computed the printed epochs
         rmse = global_rmse(eng, n_epochs, n_total, group)
     P = _gather_rows(eng.P, bounds, group)
     bu = _gather_rows(eng.bu.reshape(-1, 1), bounds, group).reshape(-1)

@@ -191,6 +191,13 @@ class StrataPlan:
         return len(self.sched)
 
     @property
+    def n_ratings(self) -> int:
+        """Ratings in the plan (positions that are not idle slots)."""
+        if getattr(self, "_n_ratings", None) is None:
+            self._n_ratings = int(np.count_nonzero(self.sched >= 0))
+        return self._n_ratings
+
+    @property
     def n_steps(self) -> np.ndarray:
         return np.diff(self.bstep)
 
@@ -255,6 +262,12 @@ class PhasedStrata:
     def serial_order(self, seq, seed) -> np.ndarray:
         parts = [ix[pl.serial_order(seq, seed)] for pl, ix in zip(self.phases, self.idx)]
         return np.concatenate(parts).astype(np.int64) if parts else np.empty(0, np.int64)
+
+    def phase_order(self, p: int, seq, seed) -> np.ndarray:
+        """Rating indices (the engine's order) that phase ``p`` alone applies
+        with strata ``seq`` and rotation ``seed`` -- one sub-epoch of the
+        rotation schedule (distributed.rotation_epoch)."""
+        return self.idx[p][self.phases[p].serial_order(seq, seed)].astype(np.int64)
 
 
 def sched_strata(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int, n_blocks: int,
@@ -454,7 +467,8 @@ class SGDEngine:
 
     def prepare_strata(self, n_blocks: Optional[int] = None,
                        waves: Optional[int] = None,
-                       phases: Optional[int] = None) -> "StrataPlan":
+                       phases: Optional[int] = None,
+                       item_bounds: Optional[np.ndarray] = None) -> "StrataPlan":
         """Build the stratified plan once and store a padded copy of the
         ratings in plan order (block-major, step-major, slot-minor).  The
         host arrays keep the original rating order.
@@ -469,12 +483,23 @@ class SGDEngine:
 
         ``phases``: item phases (PhasedStrata).  None = by the plan (env
         MF_STRATA_PHASES overrides): one phase while the default B fits one
-        workgroup per CU, else the fewest phases whose B does."""
+        workgroup per CU, else the fewest phases whose B does.
+
+        ``item_bounds``: the phases' item ranges given explicitly (len P + 1
+        ascending ids from 0 to n_items) -- the item ranges of the rotation
+        schedule (distributed.item_ranges); a PhasedStrata even for P = 1."""
         if self.colored is not None or self.strata is not None:
             raise RuntimeError("ratings already permuted by another schedule")
         env = os.environ.get("MF_STRATA_WAVES")
         if waves is None and env in ("4", "8", "16"):
             waves = int(env)
+        if item_bounds is not None:
+            ilo = np.asarray(item_bounds, np.int64)
+            if (len(ilo) < 2 or ilo[0] != 0 or ilo[-1] != self.n_items
+                    or np.any(np.diff(ilo) < 0)):
+                raise ValueError("item_bounds must ascend from 0 to n_items")
+            self.strata = self._prepare_phased(len(ilo) - 1, n_blocks, waves, ilo)
+            return self.strata
         if phases is None and os.environ.get("MF_STRATA_PHASES"):
             phases = int(os.environ["MF_STRATA_PHASES"])
         bounds = None
@@ -550,13 +575,17 @@ class SGDEngine:
         plan.narrow = waves == 4
         return plan
 
-    def _prepare_phased(self, P: int, n_blocks, waves) -> PhasedStrata:
-        ilo = balanced_bounds(self.i_host, self.n_items, P).astype(np.int64)
-        idx = [np.flatnonzero((self.i_host >= ilo[p]) & (self.i_host < ilo[p + 1]))
-               for p in range(P)]
+    def _prepare_phased(self, P: int, n_blocks, waves, ilo=None) -> PhasedStrata:
+        if ilo is None:
+            ilo = balanced_bounds(self.i_host, self.n_items, P).astype(np.int64)
+        # one pass over the ratings: each phase's indices in rating order
+        ph = np.searchsorted(ilo[1:], self.i_host, side="right")
+        order = np.argsort(ph, kind="stable")
+        cuts = np.searchsorted(ph[order], np.arange(P + 1))
+        idx = [order[cuts[p]:cuts[p + 1]] for p in range(P)]
         if n_blocks is None:                # one B for every phase: the largest needed
             n_blocks = max(choose_strata_blocks(self.u_host[ix], self.i_host[ix] - ilo[p],
-                                                self.n_users, int(ilo[p + 1] - ilo[p]),
+                                                self.n_users, max(int(ilo[p + 1] - ilo[p]), 1),
                                                 self.k, self.dcode)[0]
                            for p, ix in enumerate(idx))
         plans = []
@@ -591,7 +620,8 @@ class SGDEngine:
             return bool(self.strata_deep_pipe)
         if pl.narrow:
             return False                       # no depth-2 form of the 4-wave kernels
-        fill = self.n / max(pl.n_positions, 1)
+        n = pl.n_ratings if isinstance(pl, StrataPlan) else self.n
+        fill = n / max(pl.n_positions, 1)
         return pl.NS == strata_slots(self.k, self.dcode, 8) or fill < 0.7
 
     def epoch_strata(self, seq: Optional[np.ndarray], seed: int, lr: float, reg: float,
@@ -644,6 +674,28 @@ class SGDEngine:
                 tot_ms += ms[0]
                 launches += int(ms[1])
         return (tot_ms, launches) if timing else None
+
+    def epoch_phase(self, p: int, seq: Optional[np.ndarray], seed: int, lr: float, reg: float,
+                    update_user: bool = True, update_item: bool = True, timing=False,
+                    persistent: Optional[bool] = None):
+        """Phase ``p`` of a PhasedStrata plan alone, in place on its rows of
+        Q / b_i: one sub-epoch of the rotation schedule (distributed.py), the
+        item range this rank holds at that moment.  ``seq`` is a permutation
+        of range(B) (None: 0..B-1)."""
+        pl = self.strata
+        if not isinstance(pl, PhasedStrata):
+            raise RuntimeError("epoch_phase needs prepare_strata(item_bounds=...) or phases")
+        seq = (np.arange(pl.B, dtype=np.int32) if seq is None
+               else np.ascontiguousarray(seq, np.int32))
+        sub = pl.phases[p]
+        lo, hi = int(pl.ilo[p]), int(pl.ilo[p + 1])
+        ms = (ctypes.c_double * 2)() if timing else None
+        if sub.n_positions == 0 or hi == lo:
+            return (0.0, 0) if timing else None
+        flags = self._strata_flags(sub, persistent)
+        self._run_strata(sub, seq, seed, lr, reg, update_user, update_item, flags, ms, None,
+                         self.Q[lo:hi], self.bi[lo:hi] if self.bi is not None else None, hi - lo)
+        return (ms[0], int(ms[1])) if timing else None
 
     def _run_strata(self, pl, seq, seed, lr, reg, update_user, update_item, flags, ms, delta,
                     Q, bi, n_items):
@@ -1088,6 +1140,15 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
     colored: draws ``np.random.permutation(n_colours)`` every epoch;
     strata:  draws ``np.random.permutation(B)`` (stratum order) and a 32-bit
              colour-rotation seed every epoch.
+
+    Strata epochs run back to back with no host synchronisation: the
+    persistent sweep's error word is sticky, so it is read only where the
+    host waits anyway (the per-epoch RMSE print with ``verbose``, or the
+    RMSE read-back at the end).  If a workgroup gave up waiting (workgroups
+    not co-resident, e.g. another process holding CUs), the parameters are
+    restored from the one snapshot taken before epoch 1 and every epoch so
+    far is replayed with the same draws as one launch per stratum -- the
+    same sequential orders, hence the same result (RuntimeWarning).
     """
     if schedule == "exact":
         order = (np.arange(engine.n, dtype=np.int64) if rng_order is None
@@ -1103,6 +1164,25 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
     else:
         raise ValueError(f"schedule must be 'exact', 'colored' or 'strata', got {schedule!r}")
     train_rmse = []
+    draws = []                                    # strata: (seq, seed) per epoch
+    persistent = None                             # strata: the engine's default
+    snap0 = None
+    if schedule == "strata" and engine.strata_persistent:
+        snap0 = engine.snapshot_params()          # once: the replay's starting point
+
+    def replay_failed(upto: int) -> None:
+        """Epochs 0..upto-1 again from snap0 as per-stratum launches."""
+        nonlocal persistent
+        warnings.warn(f"the persistent strata sweep could not complete within epochs 1-{upto} "
+                      "(workgroups not co-resident); replayed them with the same draws as one "
+                      "launch per stratum", RuntimeWarning, stacklevel=3)
+        persistent = False
+        engine.restore_params(snap0)
+        engine.clear_strata_error()
+        for ep, (sq, sd) in enumerate(draws[:upto]):
+            engine.epoch_strata(sq, sd, lr, reg, update_user, update_item, persistent=False)
+            engine.sse_async(ep)
+
     for epoch in range(n_epochs):
         if schedule == "exact":
             _prep.legacy_shuffle_(order)          # = np.random.shuffle(order)
@@ -1113,17 +1193,22 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
         else:
             seq = np.random.permutation(nb).astype(np.int32)
             seed = int(np.random.randint(0, 2**31 - 1))
-            if engine.epoch_strata_checked(seq, seed, lr, reg, update_user, update_item):
-                warnings.warn(f"epoch {epoch + 1}: the persistent strata sweep could not "
-                              "complete (workgroups not co-resident); re-ran the epoch as "
-                              "one launch per stratum", RuntimeWarning, stacklevel=2)
+            draws.append((seq, seed))
+            engine.epoch_strata(seq, seed, lr, reg, update_user, update_item,
+                                persistent=persistent)
         engine.sse_async(epoch)
         if verbose == 1:
+            if snap0 is not None and persistent is None and engine.strata_failed():
+                replay_failed(epoch + 1)
             rmse = engine.rmse_values(epoch + 1)[epoch]
             train_rmse.append(rmse)
             print("Epoch ", epoch + 1, "/", n_epochs, " -  train_rmse:", rmse)
         if on_epoch is not None:
             on_epoch(epoch)
+    if snap0 is not None and persistent is None and engine.strata_failed():
+        replay_failed(n_epochs)
+        if verbose == 1:
+            train_rmse = engine.rmse_values(n_epochs)
     if verbose != 1:
         train_rmse = engine.rmse_values(n_epochs)
     return train_rmse

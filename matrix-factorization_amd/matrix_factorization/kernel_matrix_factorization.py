@@ -22,6 +22,13 @@ Three keyword arguments are new and default to the reference's behaviour:
               RCCL all-reduce of the item-row deltas once per epoch,
               distributed.fit_sharded) and every rank ends with the full
               model.  Needs schedule "strata" or "colored".
+``exchange``  process-group mode only: "rotate" (default; exact -- items are
+              cut into one range per rank and the ranges are passed round the
+              ring between sub-epochs, so every rating is applied with the
+              current user and item rows: a sequential order like the
+              single-GPU schedules) or "delta" (item-row deltas all-reduced
+              once per epoch and applied damped: faster per epoch, item
+              updates one epoch late).  DESIGN.md section 6 has both measured.
 """
 
 from __future__ import annotations
@@ -32,7 +39,7 @@ import numpy as np
 import pandas as pd
 
 from . import _lib
-from .distributed import fit_sharded, world_info
+from .distributed import EXCHANGES, fit_sharded, world_info
 from .engine import SGDEngine, canonical_dtype, fit_epochs
 from .recommender_base import RecommenderBase
 
@@ -77,7 +84,8 @@ class KernelMF(RecommenderBase):
     Arguments (reference defaults): n_factors=100, n_epochs=100,
     kernel='linear' | 'sigmoid' | 'rbf', gamma='auto' (1/n_factors, rbf
     only), reg=1, lr=0.01, init_mean=0, init_sd=0.1, min_rating=0,
-    max_rating=5, verbose=1; plus dtype, schedule, device (module docstring).
+    max_rating=5, verbose=1; plus dtype, schedule, device, distributed,
+    exchange (module docstring).
     """
 
     def __init__(self, n_factors: int = 100, n_epochs: int = 100,
@@ -85,11 +93,14 @@ class KernelMF(RecommenderBase):
                  reg: float = 1, lr: float = 0.01, init_mean: float = 0,
                  init_sd: float = 0.1, min_rating: int = 0, max_rating: int = 5,
                  verbose: int = 1, dtype: str = "float64",
-                 schedule: str = "exact", device=None, distributed: bool = False):
+                 schedule: str = "exact", device=None, distributed: bool = False,
+                 exchange: str = "rotate"):
         if kernel not in ("linear", "sigmoid", "rbf"):
             raise ValueError("Kernel must be one of linear, sigmoid, or rbf")
         if schedule not in ("exact", "colored", "strata"):
             raise ValueError("schedule must be 'exact', 'colored' or 'strata'")
+        if exchange not in EXCHANGES:
+            raise ValueError(f"exchange must be one of {EXCHANGES}")
         canonical_dtype(dtype)
         super().__init__(min_rating=min_rating, max_rating=max_rating, verbose=verbose)
         self.n_factors = n_factors
@@ -105,6 +116,7 @@ class KernelMF(RecommenderBase):
         self.schedule = schedule
         self.device = device
         self.distributed = distributed
+        self.exchange = exchange
 
     # ----------------------------------------------------- device state
     def _make_engine(self, X: pd.DataFrame) -> SGDEngine:
@@ -123,13 +135,23 @@ class KernelMF(RecommenderBase):
         self.user_biases, self.item_biases = bu, bi
         self._pred_key = self._param_key()
 
+    # predict / recommend re-check the parameter arrays' bytes on every call
+    # (in-place edits are seen, as the reference sees them); False: only a
+    # replaced array triggers a re-upload (serving a model nobody edits)
+    track_inplace_edits = True
+
     def _param_key(self):
         """What the device copies were made from: the attribute arrays (by
         identity) and a fingerprint of their bytes, so replaced arrays and
         in-place edits (``model.item_features[3] = ...``, update_users'
         row resets) are both seen -- the reference predicts from the live
-        arrays (kernel_matrix_factorization.py:148-160)."""
+        arrays (kernel_matrix_factorization.py:148-160).  The fingerprint
+        reads every parameter byte on the host (mf_fingerprint, ~10 GB/s on
+        16 threads: ~28 ms per call for a C3 model of 282 MB);
+        ``track_inplace_edits = False`` skips it."""
         arrs = (self.user_features, self.item_features, self.user_biases, self.item_biases)
+        if not self.track_inplace_edits:
+            return arrs, None
         return arrs, tuple(_fingerprint(a) for a in arrs)
 
     def _predictor(self) -> SGDEngine:
@@ -166,7 +188,7 @@ class KernelMF(RecommenderBase):
         # build-only arguments added after a pickle was written take their
         # defaults (the reference's pickles have none of them)
         for key, default in (("dtype", "float64"), ("schedule", "exact"), ("device", None),
-                             ("distributed", False)):
+                             ("distributed", False), ("exchange", "rotate")):
             state.setdefault(key, default)
         self.__dict__.update(state)
         _warn_if_no_device()
@@ -191,7 +213,7 @@ class KernelMF(RecommenderBase):
                 self.user_features, self.item_features, self.user_biases, self.item_biases,
                 self.n_epochs, self.kernel, self.n_factors, self.dtype, self.device, self.gamma,
                 self.min_rating, self.max_rating, self.global_mean, self.lr, self.reg,
-                self.schedule, verbose=self.verbose) if n else (
+                self.schedule, verbose=self.verbose, exchange=self.exchange) if n else (
                 self.user_features, self.item_features, self.user_biases, self.item_biases,
                 [float("nan")] * self.n_epochs, None)
             self.user_features, self.item_features = P, Q
@@ -209,7 +231,12 @@ class KernelMF(RecommenderBase):
         return self
 
     def predict(self, X: pd.DataFrame, bound_ratings: bool = True) -> list:
-        """kernel_matrix_factorization.py:130-163."""
+        """kernel_matrix_factorization.py:130-163.  Scores on the GPU from
+        device copies of the parameters, refreshed when the attribute arrays
+        were replaced or edited in place since the last call (a host pass
+        over the parameters per call, see _param_key; set
+        ``track_inplace_edits = False`` on a model that is not edited to skip
+        it)."""
         if X.shape[0] == 0:
             return []
         X = self._preprocess_data(X=X, type="predict")

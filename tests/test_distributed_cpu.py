@@ -46,6 +46,8 @@ class CpuEngine:
     """Test double of SGDEngine for the colored and strata schedules (oracle
     sweeps in the schedule's serial order; the plans are the product's)."""
 
+    strata_persistent = False      # no persistent sweep: nothing can give up waiting
+
     def __init__(self, u, i, r, n_users, n_items, k, mu):
         self.u_host, self.i_host, self.r_host = u, i, r
         self.n, self.n_users, self.n_items, self.k = len(u), n_users, n_items, k
@@ -77,11 +79,26 @@ class CpuEngine:
         self.colored = offs
         return len(offs) - 1
 
-    def prepare_strata(self, n_blocks=None):
-        from matrix_factorization.engine import (StrataPlan, balanced_bounds, sched_strata,
-                                                 strata_slots)
+    def prepare_strata(self, n_blocks=None, item_bounds=None):
+        from matrix_factorization.engine import (PhasedStrata, StrataPlan, balanced_bounds,
+                                                 sched_strata, strata_slots)
 
         B = STRATA_B if n_blocks is None else n_blocks
+        if item_bounds is not None:          # the product's PhasedStrata over given ranges
+            ilo = np.asarray(item_bounds, np.int64)
+            ns = strata_slots(self.k, self.dcode)
+            plans, idx = [], []
+            for p in range(len(ilo) - 1):
+                ix = np.flatnonzero((self.i_host >= ilo[p]) & (self.i_host < ilo[p + 1]))
+                uu, ii = self.u_host[ix], self.i_host[ix] - int(ilo[p])
+                m = int(ilo[p + 1] - ilo[p])
+                ub = balanced_bounds(uu, self.n_users, B)
+                ib = balanced_bounds(ii, m, B)
+                sched, bstep = sched_strata(uu, ii, self.n_users, m, B, ub, ib, ns)
+                plans.append(StrataPlan(B, ns, ub, ib, bstep, sched))
+                idx.append(ix)
+            self.strata = PhasedStrata(plans, idx, ilo)
+            return self.strata
         ub = balanced_bounds(self.u_host, self.n_users, B)
         ib = balanced_bounds(self.i_host, self.n_items, B)
         ns = strata_slots(self.k, self.dcode)
@@ -91,7 +108,7 @@ class CpuEngine:
         return self.strata
 
     def epoch_strata(self, seq, seed, lr, reg, update_user=True, update_item=True,
-                     timing=False, delta=None):
+                     timing=False, delta=None, persistent=None):
         order = self.strata.serial_order(seq, seed)
         Q0, bi0 = self.Q.clone(), self.bi.clone()
         oracle.sgd_pass(self.u_host, self.i_host, self.r_host, self.global_mean,
@@ -103,8 +120,21 @@ class CpuEngine:
             self.Q.copy_(Q0)
             self.bi.copy_(bi0)
 
+    def epoch_phase(self, c, seq, seed, lr, reg, update_user=True, update_item=True,
+                    timing=False, persistent=None):
+        order = self.strata.phase_order(c, seq, seed)
+        oracle.sgd_pass(self.u_host, self.i_host, self.r_host, self.global_mean,
+                        self.bu.numpy(), self.bi.numpy(), self.P.numpy(), self.Q.numpy(),
+                        lr=lr, reg=reg, order=order)
+
     def check_strata(self):
         pass
+
+    def strata_failed(self):
+        return False
+
+    def sse_values(self, n):
+        return self.sse_buf[:n].numpy().copy()
 
     def epoch_colored(self, seq, lr, reg, update_user=True, update_item=True, timing=False):
         order = np.concatenate([np.arange(self.colored[b], self.colored[b + 1])
@@ -266,7 +296,7 @@ def _frame():
     return pd.DataFrame({"user_id": u * 7 + 3, "item_id": i * 5 + 1}), pd.Series(r)
 
 
-def _fit_rank(rank, world, port, out_dir):
+def _fit_rank(rank, world, port, out_dir, exchange="delta"):
     """KernelMF(distributed=True).fit on every rank: the product's sharding,
     per-epoch draws, delta all-reduce and final gathers; the device sweeps
     are the CPU test double."""
@@ -280,7 +310,7 @@ def _fit_rank(rank, world, port, out_dir):
     D.ReplicaExchange = _exchange_cls()
     X, y = _frame()
     np.random.seed(SEED)
-    m = mf.KernelMF(distributed=True, **FIT_HP).fit(X, y)
+    m = mf.KernelMF(distributed=True, exchange=exchange, **FIT_HP).fit(X, y)
     np.savez(os.path.join(out_dir, f"fit{rank}.npz"), P=m.user_features, Q=m.item_features,
              bu=m.user_biases, bi=m.item_biases, rmse=np.asarray(m.train_rmse),
              uids=np.asarray(list(m.user_id_map)), iids=np.asarray(list(m.item_id_map)))
@@ -347,8 +377,8 @@ def test_kernelmf_distributed_fit_two_ranks(tmp_path):
     """The estimator's process-group mode (row 8(e) through fit()): both
     ranks end with the same full model, equal to the restated algorithm."""
     world = 2
-    mp.start_processes(_fit_rank, args=(world, _free_port(), str(tmp_path)), nprocs=world,
-                       join=True, start_method="spawn")
+    mp.start_processes(_fit_rank, args=(world, _free_port(), str(tmp_path), "delta"),
+                       nprocs=world, join=True, start_method="spawn")
     res = [dict(np.load(tmp_path / f"fit{k}.npz")) for k in range(world)]
     for key in ("P", "Q", "bu", "bi", "rmse", "uids", "iids"):
         assert np.array_equal(res[0][key], res[1][key]), key
@@ -356,3 +386,89 @@ def test_kernelmf_distributed_fit_two_ranks(tmp_path):
     for key, ref in (("P", P), ("Q", Q), ("bu", bu), ("bi", bi), ("rmse", rmse)):
         assert np.max(np.abs(res[0][key] - ref)) < 1e-12, key
     assert rmse[-1] < rmse[0]
+
+
+# ------------------------------------------------ exchange="rotate" (exact)
+def _mapped():
+    """The fit frame after the reference's preprocessing and initial draws
+    (sample, normal(P), normal(Q)): internal ids, ratings, P0, Q0."""
+    import matrix_factorization as mf
+
+    X, y = _frame()
+    np.random.seed(SEED)
+    m = mf.KernelMF(**FIT_HP)
+    Xp = m._preprocess_data(X=X, y=y, type="fit")
+    P = np.random.normal(0, 0.1, (m.n_users, K))
+    Q = np.random.normal(0, 0.1, (m.n_items, K))
+    return (Xp["user_id"].to_numpy(np.int32), Xp["item_id"].to_numpy(np.int32),
+            Xp["rating"].to_numpy(np.float64), m.n_users, m.n_items, P, Q,
+            float(Xp["rating"].mean()))
+
+
+def _replay(world):
+    """RotationReplay (the product's one-process form of the N-rank rotation)
+    on the CPU test double, with the fit's draws: (P, Q, bu, bi, rmse, draws,
+    replay)."""
+    from matrix_factorization.distributed import RotationReplay
+
+    u, i, r, nu, ni, P0, Q0, mu = _mapped()
+    rp = RotationReplay(u, i, r, nu, ni, world, K, "linear", "float64", None,
+                        global_mean=mu, engine_cls=_cpu_engine_factory)
+    rp.load(P0, Q0, np.zeros(nu), np.zeros(ni))
+    draws, sse = [], []
+    for ep in range(EPOCHS):
+        draws.append(int(np.random.randint(0, 2**31 - 1)))   # the fit's one draw per epoch
+        rp.epoch(draws[-1], LR, REG)
+        sse.append(rp.sse(ep))
+    P, Q, bu, bi = rp.params()
+    return P, Q, bu, bi, np.sqrt(np.asarray(sse) / len(u)), draws, rp
+
+
+def test_item_ranges_cover_and_balance():
+    from matrix_factorization.distributed import item_ranges
+
+    u, i, r, _, _ = _data()
+    for world in (1, 2, 3, 8):
+        b = item_ranges(i, NI, world)
+        assert b[0] == 0 and b[-1] == NI and np.all(np.diff(b) > 0)
+    # a degenerate skew (every rating on item 0) still leaves no range empty
+    b = item_ranges(np.zeros(100, np.int32), 10, 4)
+    assert b[0] == 0 and b[-1] == 10 and np.all(np.diff(b) > 0)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_rotation_epoch_is_a_sequential_sweep(world):
+    """Every rotation epoch equals the oracle's plain sequential sweep over
+    RotationReplay.serial_order (each rating once, with the current user AND
+    item rows): the exchange is exact, not an approximation."""
+    u, i, r, nu, ni, P0, Q0, mu = _mapped()
+    P, Q, bu, bi, rmse, draws, rp = _replay(world)
+    Po, Qo, buo, bio = P0.copy(), Q0.copy(), np.zeros(nu), np.zeros(ni)
+    sse = []
+    for d in draws:
+        order = rp.serial_order(d)
+        assert np.array_equal(np.sort(order), np.arange(len(u)))     # each rating once
+        oracle.sgd_pass(u, i, r, mu, buo, bio, Po, Qo, lr=LR, reg=REG, order=order)
+        sse.append(oracle.sse(u, i, r, mu, buo, bio, Po, Qo))
+    for got, ref in ((P, Po), (Q, Qo), (bu, buo), (bi, bio)):
+        assert np.max(np.abs(got - ref)) < 1e-12
+    assert np.max(np.abs(rmse - np.sqrt(np.asarray(sse) / len(u)))) < 1e-12
+    assert rmse[-1] < rmse[0]
+
+
+@pytest.mark.timeout(300)
+def test_kernelmf_distributed_rotate_two_ranks(tmp_path):
+    """KernelMF(distributed=True, exchange="rotate").fit on two gloo ranks:
+    the product's item ranges, ring hand-offs (batched send / recv) and
+    final all-gather; both ranks end with the same model, equal to the
+    one-process replay of the same draws."""
+    world = 2
+    mp.start_processes(_fit_rank, args=(world, _free_port(), str(tmp_path), "rotate"),
+                       nprocs=world, join=True, start_method="spawn")
+    res = [dict(np.load(tmp_path / f"fit{k}.npz")) for k in range(world)]
+    for key in ("P", "Q", "bu", "bi", "rmse", "uids", "iids"):
+        assert np.array_equal(res[0][key], res[1][key]), key
+    P, Q, bu, bi, rmse, _, _ = _replay(world)
+    for key, ref in (("P", P), ("Q", Q), ("bu", bu), ("bi", bi), ("rmse", rmse)):
+        assert np.max(np.abs(res[0][key] - ref)) < 1e-12, key

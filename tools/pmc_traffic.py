@@ -45,9 +45,13 @@ def main():
     ap.add_argument("--calib-write", required=True)
     ap.add_argument("--bench-fetch", required=True)
     ap.add_argument("--bench-write", required=True)
-    ap.add_argument("--key", default="c3/n1")
+    ap.add_argument("--key", default="c3/strata_persistent/float32/n1",
+                    help="workload/schedule/dtype/nN: the key bench.py looks up")
     ap.add_argument("--sgd-kernel", default="k_sgd_batch",
                     help="name fragment of the SGD kernel (k_sgd_batch | k_sgd_strata)")
+    ap.add_argument("--kernel-label", default=None,
+                    help="kernel name stored with the entry (bench.py matches it against "
+                         "the kernel its roofline names); default: --sgd-kernel")
     ap.add_argument("--out", default="profiles/traffic.json")
     ap.add_argument("--shape", default="x4", choices=["x1", "x4"],
                     help="calibration kernels matching the bench kernels' access "
@@ -75,6 +79,7 @@ def main():
     if os.path.exists(args.out):
         out = json.load(open(args.out))
     out[args.key] = {
+        "kernel": args.kernel_label or args.sgd_kernel,
         "hbm_bytes_per_sgd_launch": res["sgd"]["fetch_bytes"] + res["sgd"]["write_bytes"],
         "calibration": {"shape": args.shape, "fetch_factor": cf, "write_factor": cw,
                         "known_bytes_per_dispatch": known},
