@@ -511,6 +511,7 @@ inline bool topk_fused(int32_t amount) {
 constexpr int kMmCap = 256;              // list capacity per user and workgroup
 constexpr int kMmChunk = kWavesPerBlock * 32;   // items scored between barriers
 constexpr int kMmMaxK = 64;
+constexpr int kMmMaxSplits = 8;          // item splits (k_topk_mm_merge merges <= 8 bands)
 
 struct MmArgs {
     const int32_t* users; int32_t nq;
@@ -891,13 +892,13 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
 template <int GS>
 __global__ __launch_bounds__(kBlock) void k_topk_mm_merge(MmArgs A, int32_t* out_items,
                                                           float* out_scores) {
-    __shared__ float s_sc[4 * kMmCap];
-    __shared__ int32_t s_id[4 * kMmCap];
-    __shared__ uint64_t s_key[4 * kMmCap];
-    __shared__ int s_off[5], s_keep;
+    __shared__ float s_sc[kMmMaxSplits * kMmCap];
+    __shared__ int32_t s_id[kMmMaxSplits * kMmCap];
+    __shared__ uint64_t s_key[kMmMaxSplits * kMmCap];
+    __shared__ int s_off[kMmMaxSplits + 1], s_keep;
     const int qy = blockIdx.x, tid = threadIdx.x;
     const int lane = tid & (kWave - 1), wv = tid / kWave;
-    const int ns = A.n_splits;                       // <= 4 (topk_mm_splits)
+    const int ns = A.n_splits;                       // <= kMmMaxSplits (topk_mm_splits)
     if (tid == 0) {
         int n = 0;
         for (int x = 0; x < ns; ++x) { s_off[x] = n; n += A.part_n[(int64_t)qy * ns + x]; }
@@ -980,7 +981,7 @@ inline int topk_mm_nt() {
 inline int topk_mm_splits(int32_t nq, int32_t n_items) {
     if (const char* e = std::getenv("MF_TOPK_MM_SPLITS")) {      // probes
         const int v = std::atoi(e);
-        if (v >= 1 && v <= 4) return v;
+        if (v >= 1 && v <= kMmMaxSplits) return v;
     }
     const int nt = topk_mm_nt();
     const int64_t blocks_q = ((int64_t)nq + 32 * nt - 1) / (32 * nt);

@@ -121,11 +121,12 @@ def _gpu_replay(world, persistent=None):
     rp = RotationReplay(u, i, r, nu, ni, world, K, "linear", "float64", "cuda:0",
                         min_rating=1, max_rating=5, global_mean=mu)
     rp.load(P0, Q0, np.zeros(nu), np.zeros(ni))
-    sse = []
+    sse, draws = [], []
     for ep in range(EPOCHS):
-        rp.epoch(int(np.random.randint(0, 2**31 - 1)), LR, REG, persistent=persistent)
+        draws.append(int(np.random.randint(0, 2**31 - 1)))
+        rp.epoch(draws[-1], LR, REG, persistent=persistent)
         sse.append(rp.sse(ep))
-    return rp.params() + (np.sqrt(np.asarray(sse) / len(u)),)
+    return rp.params() + (np.sqrt(np.asarray(sse) / len(u)), rp, draws)
 
 
 @pytest.mark.timeout(600)
@@ -134,9 +135,10 @@ def test_kernelmf_distributed_rotate_on_one_gpu(tmp_path):
     sharing cuda:0: item ranges handed round the ring (staged through host
     memory under gloo), final all-gather; both ranks equal, bit-equal to the
     one-GPU RotationReplay of the same draws, and equal to the oracle's
-    sequential sweep of the stated serial order (test_distributed_cpu's CPU
-    replay) to FP64 rounding."""
-    from test_distributed_cpu import _free_port, _replay
+    sequential sweep of that replay's stated serial order to FP64
+    rounding."""
+    import oracle
+    from test_distributed_cpu import EPOCHS, LR, REG, _free_port, _mapped
 
     world = 2
     mp.start_processes(_fit_rank_rotate, args=(world, _free_port(), str(tmp_path)),
@@ -144,12 +146,20 @@ def test_kernelmf_distributed_rotate_on_one_gpu(tmp_path):
     res = [dict(np.load(tmp_path / f"rot{k}.npz")) for k in range(world)]
     for key in ("P", "Q", "bu", "bi", "rmse"):
         assert np.array_equal(res[0][key], res[1][key]), key
-    P, Q, bu, bi, rmse = _gpu_replay(world)
+    P, Q, bu, bi, rmse, rp, draws = _gpu_replay(world)
     for key, ref in (("P", P), ("Q", Q), ("bu", bu), ("bi", bi)):
         assert np.array_equal(res[0][key], ref), key
     assert np.max(np.abs(res[0]["rmse"] - rmse)) < 1e-13
-    Pc, Qc, buc, bic, rmc, _, _ = _replay(world)
-    for key, ref in (("P", Pc), ("Q", Qc), ("bu", buc), ("bi", bic), ("rmse", rmc)):
+    u, i, r, nu, ni, Po, Qo, mu = _mapped()
+    buo, bio, sse = np.zeros(nu), np.zeros(ni), []
+    for d in draws:
+        order = rp.serial_order(d)
+        assert np.array_equal(np.sort(order), np.arange(len(u)))
+        oracle.sgd_pass(u, i, r, mu, buo, bio, Po, Qo, lr=LR, reg=REG, order=order)
+        sse.append(oracle.sse(u, i, r, mu, buo, bio, Po, Qo))
+    rmo = np.sqrt(np.asarray(sse) / len(u))
+    assert EPOCHS == len(draws)
+    for key, ref in (("P", Po), ("Q", Qo), ("bu", buo), ("bi", bio), ("rmse", rmo)):
         assert np.max(np.abs(res[0][key] - ref)) < 1e-10, key
 
 

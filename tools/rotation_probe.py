@@ -41,9 +41,10 @@ def log(msg):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c3")
-    ap.add_argument("--worlds", default="2,4,8")
+    ap.add_argument("--worlds", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--epochs", type=int, default=20)
-    ap.add_argument("--blocks", default="", help="comma list of B per rank (empty = default rule)")
+    ap.add_argument("--blocks", type=int, nargs="*", default=[],
+                    help="B values per rank to sweep (none = the default rule)")
     ap.add_argument("--waves", type=int, default=None)
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--reg", type=float, default=0.02)
@@ -99,8 +100,8 @@ def main():
         del e1
         torch.cuda.empty_cache()
 
-    blocks = [int(b) for b in args.blocks.split(",") if b] or [None]
-    for W in [int(w) for w in args.worlds.split(",")]:
+    blocks = list(args.blocks) or [None]
+    for W in args.worlds:
         for B in blocks:
             t0 = time.time()
             rp = RotationReplay(u, i, r, nu, ni, W, k, kernel, "float32", dev, n_blocks=B,

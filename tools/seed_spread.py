@@ -1,0 +1,138 @@
+#!/usr/bin/env python
+"""How far apart do two equally valid SGD orders end after E epochs?
+
+The reference's own visit order is random every run (numba's shuffle is
+seeded from os.urandom: SURVEY 8(c)), so its final training RMSE has a
+run-to-run spread; a build's RMSE "matches the reference" only up to that.
+This probe measures it on the bench workload, from the bench's start
+(bench.synth, RandomState(7) normals, zero biases), all on one GPU in FP32:
+
+  exact    the reference's order: np.random.shuffle of the rating rows every
+           epoch (kernel_matrix_factorization.py:369-371), applied exactly
+           (level schedule, engine.epoch_exact) -- one run per --shuffle-seeds
+           entry (np.random.seed(s) before the first epoch);
+  strata   the single-GPU throughput schedule, one run per --draw-seeds entry
+           (stratum orders and rotations drawn from that seed);
+  rotate   the N-GPU rotation order (distributed.RotationReplay), one run per
+           --draw-seeds entry, for each N in --worlds.
+
+Prints / writes one JSON document: per run the RMSE of every epoch; per
+family the spread (max - min) of the final RMSE and the mean.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "matrix-factorization_amd"))
+sys.path.insert(0, ROOT)
+
+
+def log(msg):
+    print(f"[seed_spread {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="c3")
+    ap.add_argument("--epochs", type=int, default=20)
+    ap.add_argument("--shuffle-seeds", type=int, nargs="*", default=[7, 8])
+    ap.add_argument("--draw-seeds", type=int, nargs="*", default=[0, 1, 2])
+    ap.add_argument("--worlds", type=int, nargs="*", default=[8])
+    ap.add_argument("--lr", type=float, default=0.01)
+    ap.add_argument("--reg", type=float, default=0.02)
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+
+    import torch
+
+    import bench
+    from matrix_factorization import _prep
+    from matrix_factorization.distributed import RotationReplay
+    from matrix_factorization.engine import SGDEngine
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    nu, ni, nnz, k, kernel, desc = bench.WORKLOADS[args.workload]
+    u, i, r = bench.synth(nu, ni, nnz)
+    mu = float(np.mean(r, dtype=np.float64))
+    rs = np.random.RandomState(7)
+    P0 = rs.normal(0.0, 0.1, (nu, k)).astype("float32")
+    Q0 = rs.normal(0.0, 0.1, (ni, k)).astype("float32")
+    hyp = dict(gamma=1.0 / k, min_rating=1.0, max_rating=5.0, global_mean=mu)
+    E = args.epochs
+    runs = []
+
+    def fresh():
+        e = SGDEngine(u, i, r, nu, ni, k, kernel, "float32", dev, **hyp)
+        e.load_params(P=P0, Q=Q0, bu=np.zeros(nu), bi=np.zeros(ni))
+        return e
+
+    for s in args.shuffle_seeds:
+        t0 = time.time()
+        e = fresh()
+        np.random.seed(s)
+        order = np.arange(nnz, dtype=np.int64)
+        for ep in range(E):
+            _prep.legacy_shuffle_(order)           # = np.random.shuffle(order), :371
+            e.epoch_exact(order, args.lr, args.reg)
+            e.sse_async(ep)
+            if ep % 5 == 4:
+                log(f"exact seed {s}: epoch {ep + 1}/{E} ({time.time() - t0:.0f}s)")
+        rm = e.rmse_values(E)
+        runs.append({"family": "exact", "seed": s, "rmse": rm, "s": time.time() - t0})
+        log(f"exact seed {s}: final {rm[-1]:.7f} in {time.time() - t0:.0f}s")
+        del e
+        torch.cuda.empty_cache()
+
+    for s in args.draw_seeds:
+        e = fresh()
+        pl = e.prepare_strata()
+        for ep in range(E):
+            rsd = np.random.RandomState([s, ep])
+            e.epoch_strata(rsd.permutation(pl.B).astype(np.int32),
+                           int(rsd.randint(0, 2**31 - 1)), args.lr, args.reg)
+            e.sse_async(ep)
+        rm = e.rmse_values(E)
+        runs.append({"family": "strata", "seed": s, "rmse": rm})
+        log(f"strata seed {s}: final {rm[-1]:.7f}")
+        del e
+        torch.cuda.empty_cache()
+
+    for W in args.worlds:
+        rp = RotationReplay(u, i, r, nu, ni, W, k, kernel, "float32", dev, **hyp)
+        for s in args.draw_seeds:
+            rp.load(P0, Q0, np.zeros(nu), np.zeros(ni))
+            rm = []
+            for ep in range(E):
+                rp.epoch(int(np.random.RandomState([s, ep, W]).randint(0, 2**31 - 1)),
+                         args.lr, args.reg)
+                rm.append(float(np.sqrt(rp.sse(ep) / nnz)))
+            runs.append({"family": f"rotate_n{W}", "seed": s, "rmse": rm})
+            log(f"rotate N={W} seed {s}: final {rm[-1]:.7f}")
+        del rp
+        torch.cuda.empty_cache()
+
+    fam = {}
+    for run in runs:
+        fam.setdefault(run["family"], []).append(run["rmse"][-1])
+    summary = {f: {"n": len(v), "mean_final": float(np.mean(v)),
+                   "spread_final": float(np.max(v) - np.min(v)), "finals": v}
+               for f, v in fam.items()}
+    doc = {"workload": desc, "epochs": E, "lr": args.lr, "reg": args.reg,
+           "summary": summary, "runs": runs}
+    txt = json.dumps(doc)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(txt)
+    print(txt)
+    log(json.dumps(summary))
+
+
+if __name__ == "__main__":
+    main()
