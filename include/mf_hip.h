@@ -152,8 +152,10 @@ size_t mf_sgd_workspace_bytes(int32_t n_launch);
  * applied the same user range (bounded wait; on timeout it sets an error
  * flag that mf_strata_status reports); it needs workspace (DEVICE, >=
  * mf_strata_workspace_bytes(n_blocks, n_seq) bytes, zero-initialised once by
- * the caller) and is used only when all n_blocks workgroups fit on the device
- * at once, else the call falls back to one launch per stratum.  The result
+ * the caller -- and zeroed WHOLE again after a reported failure, since the
+ * position counters in it grow across launches) and is used only when
+ * n_seq <= 256 and all n_blocks workgroups fit on the device at once, else
+ * the call falls back to one launch per stratum.  The result
  * is the same sequential order either way.  kernel_ms (HOST, optional):
  * elapsed ms of the whole call and the launch count (synchronises).
  */

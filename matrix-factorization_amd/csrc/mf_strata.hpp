@@ -529,11 +529,20 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata(StrataArgs<T> A) {
 // error flag is set and the workgroup leaves, so the grid always drains).
 constexpr int64_t kStrataSpinLimit = (int64_t)1 << 24;
 
+// The stratum order of one persistent launch travels in the kernel arguments
+// (no host-to-device copy per launch): at most one stratum per workgroup, and
+// the persistent kernel runs one workgroup per CU.
+constexpr int kStrataSeqArg = 256;
+struct StrataSeq { int32_t s[kStrataSeqArg]; };
+
 // The whole epoch in one launch (MF_FLAG_PERSISTENT): workgroup w keeps item
 // slab w in LDS for every stratum and walks the strata of `seq`; before
 // position t it waits until the workgroup that applied position t - 1 to the
 // same user range, w' = (w + seq[t] - seq[t-1]) mod B, has published
-// done[w'] >= t.  Hand-off (cdna_hip_programming.md Guideline 16, R1): the
+// done[w'] >= base + t.  The counters only grow (no reset per launch): every
+// workgroup ends a launch at the same count, so each reads its own counter at
+// the start as `base` (zeroed once with the workspace, and again whenever
+// the caller clears the error word).  Hand-off (cdna_hip_programming.md Guideline 16, R1): the
 // block's user rows and user-bias slice are stored write-through (sc1), every
 // storing wave drains (vmcnt(0)), a barrier, one relaxed agent-scope flag
 // store; the consumer polls relaxed and reads every handed-off byte with sc1
@@ -545,15 +554,17 @@ constexpr int64_t kStrataSpinLimit = (int64_t)1 << 24;
 // then runs as one launch per stratum).
 template <typename T, int W, int GS, int V, int KERN, int S, int DEPTH = 1, int NW = kStrataWaves>
 __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A,
-                                                                    const int32_t* seq,
+                                                                    const StrataSeq seq,
                                                                     int32_t n_seq, int32_t* done,
                                                                     int32_t* err) {
     constexpr int TH = NW * kWave;
     extern __shared__ __align__(16) unsigned char smem[];
-    __shared__ int s_abort;
+    __shared__ int s_abort, s_base;
     const int B = A.B;
     const int w = blockIdx.x;
     const int ilo = A.ibnd[w], nqi = A.ibnd[w + 1] - ilo;
+    if (threadIdx.x == 0)                 // this workgroup's count at the end of the last launch
+        s_base = __hip_atomic_load(done + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     T* Qs = reinterpret_cast<T*>(smem);
     T* Bis = Qs + (size_t)nqi * A.k;
     T* Bus = Bis + nqi;
@@ -565,17 +576,20 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
         if (A.probe && threadIdx.x == 0)
             A.probe[((int64_t)t * B + w) * 4 + q] = (int64_t)__builtin_amdgcn_s_memrealtime();
     };
+    __syncthreads();
+    const int base = s_base;
     for (int t = 0; t < n_seq; ++t) {
-        const int s = seq[t];
+        const int s = seq.s[t];
         const int ub = (w + s) % B;
         const int ulo = A.ubnd[ub], nus = A.ubnd[ub + 1] - ulo;
         stamp(t, 0);
         if (threadIdx.x == 0) {
             int ab = 0;
             if (t > 0) {
-                const int wd = (w + s - seq[t - 1] + 2 * B) % B;
+                const int wd = (w + s - seq.s[t - 1] + 2 * B) % B;
                 int64_t spins = 0;
-                while (__hip_atomic_load(done + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < t) {
+                while (__hip_atomic_load(done + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                       base + t) {
                     __builtin_amdgcn_s_sleep(2);
                     if (++spins > kStrataSpinLimit ||
                         __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
@@ -609,7 +623,7 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0)
-            __hip_atomic_store(done + w, t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done + w, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         stamp(t, 3);
     }
     __syncthreads();
@@ -635,7 +649,9 @@ struct StrataParams {
     int64_t n_items; void* dq; void* dbi;    // delta-out (nullable)
 };
 
-// workspace of the persistent kernel: done[B], err, seq[n_seq] (int32)
+// workspace of the persistent kernel (int32): done[B] (position counters,
+// growing across launches), err, then n_seq words no longer used (the
+// stratum order travels in the kernel arguments; the size is kept for the ABI)
 inline size_t strata_ws_bytes(int32_t B, int32_t n_seq) {
     return sizeof(int32_t) * ((size_t)B + 1 + (size_t)n_seq);
 }
@@ -761,7 +777,7 @@ struct StrataRun {
             MF_HIP_CHECK(hipEventRecord(ev[0], p.stream));
         }
         bool persistent = false;
-        if ((p.flags & MF_FLAG_PERSISTENT) && p.ws &&
+        if ((p.flags & MF_FLAG_PERSISTENT) && p.ws && p.n_seq <= kStrataSeqArg &&
             p.ws_bytes >= strata_ws_bytes(p.B, p.n_seq) && a.p_bytes < (uint64_t)kBufDrop) {
             // (the deep pipeline exists for the 16- and 8-wave kernels)
             constexpr int kDeep = NW >= 8 ? 2 : 1;
@@ -774,22 +790,20 @@ struct StrataRun {
             if (persistent) {
                 int32_t* done = static_cast<int32_t*>(p.ws);
                 int32_t* err = done + p.B;
-                const int32_t* dseq = err + 1;
                 int32_t nseq = p.n_seq;
-                MF_HIP_CHECK(hipMemsetAsync(done, 0, sizeof(int32_t) * (size_t)p.B, p.stream));
+                StrataSeq sq;
+                for (int32_t t = 0; t < kStrataSeqArg; ++t) sq.s[t] = t < nseq ? p.seq[t] : 0;
                 if (strata_inject_fail())
                     MF_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(err), 1, 1,
                                                    p.stream));
-                MF_HIP_CHECK(hipMemcpyAsync(err + 1, p.seq, sizeof(int32_t) * (size_t)p.n_seq,
-                                            hipMemcpyHostToDevice, p.stream));
                 if (p.flags & MF_FLAG_NO_COOP) {
                     hipLaunchKernelGGL(efn, dim3((unsigned)p.B), dim3(TH), lds,
-                                       p.stream, a, dseq, nseq, done, err);
+                                       p.stream, a, sq, nseq, done, err);
                 } else {
                     // cooperative: the runtime guarantees that all B workgroups
                     // are resident at once (the neighbour waits need it) or
                     // refuses the launch -- then one launch per stratum below
-                    void* kargs[] = {&a, &dseq, &nseq, &done, &err};
+                    void* kargs[] = {&a, &sq, &nseq, &done, &err};
                     const hipError_t ce = hipLaunchCooperativeKernel(
                         reinterpret_cast<const void*>(efn), dim3((unsigned)p.B),
                         dim3(TH), kargs, (unsigned)lds, p.stream);

@@ -304,12 +304,21 @@ def strata_slots(k: int, dcode: int, waves: int = 16) -> int:
     return ns
 
 
-def choose_strata_blocks(u, i, n_users, n_items, k, dcode, max_blocks=None):
-    """B and the user / item bounds: B ~ sqrt(n / 1024) capped at 256 (one
+# ratings per B^2 of the default plan rule B = sqrt(n / STRATA_PER_B2): the
+# single-GPU epoch (C3 caps at 256, C2 gives 69; DESIGN.md section 5 sweeps)
+STRATA_PER_B2 = 1024.0
+# the same for one rank's sub-block of the rotation schedule (n / N^2 ratings:
+# fewer ratings per block pay, DESIGN.md section 6 sweeps)
+ROTATE_PER_B2 = 1024.0
+
+
+def choose_strata_blocks(u, i, n_users, n_items, k, dcode, max_blocks=None,
+                         per_b2: float = STRATA_PER_B2):
+    """B and the user / item bounds: B ~ sqrt(n / per_b2) capped at 256 (one
     workgroup per CU), raised until the largest block's LDS image fits."""
     lib = _lib.load()
     n = len(u)
-    B = int(min(256, max(1, np.sqrt(n / 1024.0))))
+    B = int(min(256, max(1, np.sqrt(n / float(per_b2)))))
     if max_blocks is not None:
         B = min(B, int(max_blocks))
     limit = lib.mf_strata_lds_limit()
@@ -498,7 +507,8 @@ class SGDEngine:
             if (len(ilo) < 2 or ilo[0] != 0 or ilo[-1] != self.n_items
                     or np.any(np.diff(ilo) < 0)):
                 raise ValueError("item_bounds must ascend from 0 to n_items")
-            self.strata = self._prepare_phased(len(ilo) - 1, n_blocks, waves, ilo)
+            self.strata = self._prepare_phased(len(ilo) - 1, n_blocks, waves, ilo,
+                                               per_b2=ROTATE_PER_B2)
             return self.strata
         if phases is None and os.environ.get("MF_STRATA_PHASES"):
             phases = int(os.environ["MF_STRATA_PHASES"])
@@ -575,7 +585,8 @@ class SGDEngine:
         plan.narrow = waves == 4
         return plan
 
-    def _prepare_phased(self, P: int, n_blocks, waves, ilo=None) -> PhasedStrata:
+    def _prepare_phased(self, P: int, n_blocks, waves, ilo=None,
+                        per_b2: float = STRATA_PER_B2) -> PhasedStrata:
         if ilo is None:
             ilo = balanced_bounds(self.i_host, self.n_items, P).astype(np.int64)
         # one pass over the ratings: each phase's indices in rating order
@@ -586,7 +597,7 @@ class SGDEngine:
         if n_blocks is None:                # one B for every phase: the largest needed
             n_blocks = max(choose_strata_blocks(self.u_host[ix], self.i_host[ix] - ilo[p],
                                                 self.n_users, max(int(ilo[p + 1] - ilo[p]), 1),
-                                                self.k, self.dcode)[0]
+                                                self.k, self.dcode, per_b2=per_b2)[0]
                            for p, ix in enumerate(idx))
         plans = []
         for p, ix in enumerate(idx):
@@ -703,11 +714,12 @@ class SGDEngine:
         old = getattr(self, "_strata_ws", None)
         if old is None or old.numel() * 4 < wsb:
             # zeroed once: the error flag (int32 at index B) is sticky until
-            # check_strata() raises or clear_strata_error() resets it; a
-            # grown workspace carries a pending error over
+            # check_strata() raises or clear_strata_error() resets it, and
+            # the position counters done[0:B] grow across launches; a grown
+            # workspace carries both over
             ws = torch.zeros((wsb + 3) // 4, dtype=torch.int32, device=self.dev)
             if old is not None:
-                ws[pl.B] = old[pl.B]
+                ws[: pl.B + 1] = old[: pl.B + 1]
             self._strata_ws = ws
         args = (_tp(pl.d_u), _tp(pl.d_i), _tp(pl.d_r),
                 pl.n_positions, pl.B, _tp(pl.d_ubnd), _tp(pl.d_ibnd), _tp(pl.d_bstep),
@@ -740,9 +752,12 @@ class SGDEngine:
         return ws is not None and int(ws[self.strata.B].item()) != 0
 
     def clear_strata_error(self) -> None:
+        """Reset the workspace after a failed persistent sweep: the error word
+        and the position counters (they grow across launches and are left
+        uneven by workgroups that gave up)."""
         ws = getattr(self, "_strata_ws", None)
         if ws is not None:
-            ws[self.strata.B] = 0
+            ws.zero_()
 
     def snapshot_params(self):
         """Device copies of (P, Q, b_u, b_i) (restore_params puts them back)."""

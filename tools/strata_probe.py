@@ -2,7 +2,10 @@
 """Phase stamps of the persistent strata kernel (mf_strata_set_probe):
 per (position t, workgroup w) the wait for the user range, the block's
 steps, the hand-off signal; mean and spread over one epoch.
-Usage: python tools/strata_probe.py [--workload c2] [--blocks B]"""
+Usage: python tools/strata_probe.py [--workload c2] [--blocks B] [--rotate N]
+--rotate N: one sub-epoch of the N-rank rotation schedule instead -- rank 0's
+users x item range 0 (distributed.shard_users / item_ranges), i.e. one
+launch of engine.epoch_phase."""
 import argparse
 import ctypes
 import os
@@ -24,26 +27,42 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c2")
     ap.add_argument("--blocks", type=int, default=None)
+    ap.add_argument("--rotate", type=int, default=0)
     args = ap.parse_args()
     nu, ni, nnz, k, kernel, _ = bench.WORKLOADS[args.workload]
     u, i, r = bench.synth(nu, ni, nnz)
+    mu = float(r.mean())
+    if args.rotate:
+        from matrix_factorization.distributed import item_ranges, local_shard, shard_users
+        bounds = shard_users(u, nu, args.rotate)
+        ilo = item_ranges(i, ni, args.rotate)
+        u, i, r = local_shard(u, i, r, bounds, 0)
+        nu = int(bounds[1])
     eng = SGDEngine(u, i, r, nu, ni, k, kernel, "float32", "cuda:0", gamma=1.0 / k,
-                    min_rating=1, max_rating=5, global_mean=float(r.mean()))
-    plan = eng.prepare_strata(n_blocks=args.blocks)
+                    min_rating=1, max_rating=5, global_mean=mu)
+    plan = eng.prepare_strata(n_blocks=args.blocks,
+                              item_bounds=ilo if args.rotate else None)
     B = plan.B
     rs = np.random.RandomState(0)
     eng.load_params(rs.normal(0, 0.1, (nu, k)).astype(np.float32),
                     rs.normal(0, 0.1, (ni, k)).astype(np.float32),
                     np.zeros(nu, np.float32), np.zeros(ni, np.float32))
+
+    def run(seq, seed):
+        if args.rotate:
+            eng.epoch_phase(0, seq, seed, 0.01, 0.02)
+        else:
+            eng.epoch_strata(seq, seed, 0.01, 0.02)
+
     for ep in range(2):
-        eng.epoch_strata(rs.permutation(B).astype(np.int32), ep, 0.01, 0.02)
+        run(rs.permutation(B).astype(np.int32), ep)
     torch.cuda.synchronize()
     probe = torch.zeros(4 * B * B, dtype=torch.int64, device="cuda:0")
     _lib.call("mf_strata_set_probe", ctypes.c_void_p(probe.data_ptr()))
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
     t0.record()
-    eng.epoch_strata(rs.permutation(B).astype(np.int32), 7, 0.01, 0.02)
+    run(rs.permutation(B).astype(np.int32), 7)
     t1.record()
     torch.cuda.synchronize()
     _lib.call("mf_strata_set_probe", None)
@@ -57,8 +76,10 @@ def main():
     sig = st[:, :, 3] - st[:, :, 2]
     gap = st[1:, :, 0] - st[:-1, :, 3]
     span = st[:, :, 3].max() - st[:, :, 0].min()
-    steps = np.diff(plan.bstep).reshape(B, B)            # [s, w]
-    print(f"{args.workload}: B={B} NS={plan.NS} epoch kernel {t0.elapsed_time(t1):.3f} ms, "
+    pl0 = plan.phases[0] if args.rotate else plan
+    steps = np.diff(pl0.bstep).reshape(B, B)             # [s, w]
+    print(f"{args.workload}{' rotate N=%d sub-epoch' % args.rotate if args.rotate else ''}: "
+          f"B={B} NS={plan.NS} epoch kernel {t0.elapsed_time(t1):.3f} ms, "
           f"stamp span {span / 1e3:.3f} ms, per position {span / B:.2f} us")
     for name, a in (("wait", wait), ("block", block), ("signal", sig), ("gap", gap)):
         print(f"  {name:6s} mean {a.mean():7.2f} us  p50 {np.median(a):7.2f}  p90 "
