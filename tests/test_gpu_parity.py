@@ -385,3 +385,28 @@ def test_topk_mfma_filter_ties_and_overflow():
     assert np.array_equal(ms, es)
     ids, sc = eng.topk(users, 64)
     assert np.array_equal(ids, ei)
+
+
+@pytest.mark.parametrize("mfma", [True, False])
+def test_topk_unsorted_exclusions(mfma):
+    """The ABI wants each user's exclusion list sorted ascending (the kernels
+    binary-search it, include/mf_hip.h); engine.topk_prepare sorts whatever
+    the caller passes, so shuffled lists give the sorted lists' result on the
+    MFMA filter and the exact fused path alike, and no excluded item comes
+    back."""
+    k, nu, ni, amount = 32, 300, 4000, 10
+    eng = _topk_engine(k, nu, ni, 11)
+    eng.topk_mfma = mfma
+    rs = np.random.RandomState(2)
+    users = rs.choice(nu, 120, replace=False).astype(np.int32)
+    cnt = rs.randint(0, 300, len(users))
+    ex_ptr = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64)
+    srt = np.concatenate([np.sort(rs.choice(ni, c, replace=False)) for c in cnt]).astype(np.int32)
+    shuf = srt.copy()
+    for q in range(len(users)):
+        rs.shuffle(shuf[ex_ptr[q]:ex_ptr[q + 1]])
+    a_i, a_s = eng.topk(users, amount, ex_ptr, srt)
+    b_i, b_s = eng.topk(users, amount, ex_ptr, shuf)
+    assert np.array_equal(a_i, b_i) and np.array_equal(a_s, b_s)
+    for q in range(len(users)):
+        assert not set(b_i[q]) & set(srt[ex_ptr[q]:ex_ptr[q + 1]])

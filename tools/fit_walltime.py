@@ -59,7 +59,35 @@ def main():
 
     KernelMF._preprocess_data = timed("preprocess", KernelMF._preprocess_data)
     KernelMF._make_engine = timed("engine_upload", KernelMF._make_engine)
-    kmf.fit_epochs = timed("epochs_incl_plan", kmf.fit_epochs)
+    # per-epoch hipEvents on the launch stream (recorded by fit_epochs'
+    # on_epoch hook: no synchronisation inside the loop)
+    ep_events = []
+    inner = kmf.fit_epochs
+
+    def with_events(*a, **kw):
+        ev0 = torch.cuda.Event(enable_timing=True)
+
+        def on_epoch(ep):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            ep_events.append(e)
+
+        orig_prepare = SGDEngine.prepare_strata
+        eng = a[0]
+
+        def prep_then_mark(*pa, **pk):          # epoch 1 starts after the plan build
+            out = orig_prepare(eng, *pa, **pk)
+            ev0.record()
+            return out
+        eng.prepare_strata = prep_then_mark
+        try:
+            out = inner(*a, on_epoch=on_epoch, **kw)
+        finally:
+            del eng.prepare_strata
+        ep_events.insert(0, ev0)
+        return out
+
+    kmf.fit_epochs = timed("epochs_incl_plan", with_events)
     SGDEngine.prepare_strata = timed("strata_plan", SGDEngine.prepare_strata)
     SGDEngine.snapshot_params = timed("start_snapshot", SGDEngine.snapshot_params)
     KernelMF._sync_params = timed("download", KernelMF._sync_params)
@@ -75,6 +103,7 @@ def main():
               - phases.get("start_snapshot", 0.0))
     phases["init_normal_and_other"] = total - sum(
         v for k, v in phases.items() if k not in ("strata_plan", "start_snapshot"))
+    ep_ms = [a.elapsed_time(b) for a, b in zip(ep_events[:-1], ep_events[1:])]
     print(json.dumps({"what": "KernelMF.fit wall time", "nnz": args.nnz,
                       "n_users": m.n_users, "n_items": m.n_items, "epochs": args.epochs,
                       "prep_path": "pandas" if args.pandas_prep else "native",
@@ -85,6 +114,12 @@ def main():
                                      "start snapshot: the epochs' SGD sweeps + RMSE passes + "
                                      "the final RMSE read-back, no per-epoch host sync"),
                       "phases_s": {k: round(v, 3) for k, v in phases.items()},
+                      "epoch_ms_events": ep_ms,
+                      "epoch_ms_events_note": ("hipEvents between consecutive epochs of "
+                                               "fit_epochs (SGD sweep + RMSE pass each); "
+                                               "epoch 1 includes the first launches"),
+                      "epoch_ms_median_2_on": float(np.median(ep_ms[1:])) if len(ep_ms) > 1
+                                              else None,
                       "final_train_rmse": float(m.train_rmse[-1]),
                       "synth_s": round(t_synth, 1)}))
 
