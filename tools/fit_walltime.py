@@ -104,6 +104,20 @@ def main():
     phases["init_normal_and_other"] = total - sum(
         v for k, v in phases.items() if k not in ("strata_plan", "start_snapshot"))
     ep_ms = [a.elapsed_time(b) for a, b in zip(ep_events[:-1], ep_events[1:])]
+    # the bench's timed loop (bench.py: epoch_strata + sse_async, events
+    # around the whole step) on the SAME engine and plan after fit(): tells
+    # fit()'s loop apart from the data layout it trains on
+    eng = m._pred_engine
+    same = []
+    for ep in range(10):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        eng.epoch_strata(bench.strata_seq(ep, eng.strata.B), bench.strata_rot(ep), 0.01, 0.02)
+        eng.sse_async(ep)
+        b.record()
+        same.append((a, b))
+    torch.cuda.synchronize()
+    same_ms = [a.elapsed_time(b) for a, b in same][1:]
     print(json.dumps({"what": "KernelMF.fit wall time", "nnz": args.nnz,
                       "n_users": m.n_users, "n_items": m.n_items, "epochs": args.epochs,
                       "prep_path": "pandas" if args.pandas_prep else "native",
@@ -120,6 +134,10 @@ def main():
                                                "epoch 1 includes the first launches"),
                       "epoch_ms_median_2_on": float(np.median(ep_ms[1:])) if len(ep_ms) > 1
                                               else None,
+                      "bench_loop_same_engine_ms_median": float(np.median(same_ms)),
+                      "bench_loop_note": ("bench.py's step (epoch_strata + sse_async) run 10x "
+                                          "on fit()'s own engine and plan afterwards, epochs "
+                                          "2-10"),
                       "final_train_rmse": float(m.train_rmse[-1]),
                       "synth_s": round(t_synth, 1)}))
 
