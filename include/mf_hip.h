@@ -254,6 +254,20 @@ int mf_sse(const int32_t* user_ids, const int32_t* item_ids,
            double min_rating, double max_rating,
            const int64_t* slice_offsets, int32_t n_slices, void* workspace,
            double* sse_out, void* stream);
+/* mf_sse with its grid capped at max_blocks workgroups of 256 threads (0 = no
+ * cap; at least n_slices): the pass then leaves CUs free for a kernel running
+ * beside it on another stream (the rotation schedule runs epoch e's RMSE
+ * beside epoch e+1's sub-epochs).  The same sum up to
+ * FP64 rounding (another grouping of the per-workgroup partial sums). */
+int mf_sse_capped(const int32_t* user_ids, const int32_t* item_ids,
+                  const void* ratings, int64_t n_ratings, double global_mean,
+                  const void* user_biases, const void* item_biases,
+                  const void* user_features, const void* item_features,
+                  int32_t n_users, int32_t n_items,
+                  int32_t n_factors, int32_t kernel, int32_t dtype, double gamma,
+                  double min_rating, double max_rating,
+                  const int64_t* slice_offsets, int32_t n_slices, void* workspace,
+                  int32_t max_blocks, double* sse_out, void* stream);
 
 /*
  * Predictions for (user, item) pairs -- replaces `_predict`

@@ -1094,6 +1094,7 @@ struct SseParams {
     int32_t n_users, n_items;
     int32_t k; int32_t kernel; double gamma, lo, hi;
     double* partials; double* sse_out; hipStream_t stream; SliceTab S;
+    int32_t max_blocks;      // > 0: at most this many workgroups (mf_sse_capped)
 };
 
 template <typename T>
@@ -1279,6 +1280,7 @@ struct SseRun {
             const int v = std::atoi(e);
             if (v > 0) blocks = std::min(v, kSseMaxBlocks);
         }
+        if (p.max_blocks > 0) blocks = std::min(blocks, p.max_blocks);
         blocks = std::max(p.S.n, (blocks / p.S.n) * p.S.n);
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(kBlock), 0, p.stream, a, p.S);
         hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(kBlock), 0, p.stream,

@@ -424,15 +424,15 @@ extern "C" size_t mf_sse_workspace_bytes(int64_t n_ratings) {
     return sizeof(double) * (size_t)kSseMaxBlocks;
 }
 
-extern "C" int mf_sse(const int32_t* user_ids, const int32_t* item_ids,
-                      const void* ratings, int64_t n_ratings,
-                      double global_mean, const void* user_biases,
-                      const void* item_biases, const void* user_features,
-                      const void* item_features, int32_t n_users, int32_t n_items,
-                      int32_t n_factors, int32_t kernel, int32_t dtype, double gamma,
-                      double min_rating, double max_rating,
-                      const int64_t* slice_offsets, int32_t n_slices, void* workspace,
-                      double* sse_out, void* stream) {
+extern "C" int mf_sse_capped(const int32_t* user_ids, const int32_t* item_ids,
+                             const void* ratings, int64_t n_ratings,
+                             double global_mean, const void* user_biases,
+                             const void* item_biases, const void* user_features,
+                             const void* item_features, int32_t n_users, int32_t n_items,
+                             int32_t n_factors, int32_t kernel, int32_t dtype, double gamma,
+                             double min_rating, double max_rating,
+                             const int64_t* slice_offsets, int32_t n_slices, void* workspace,
+                             int32_t max_blocks, double* sse_out, void* stream) {
     if (n_ratings < 0 || !sse_out || !workspace || n_users < 0 || n_items < 0 ||
         (slice_offsets && (n_slices < 1 || n_slices > kMaxSlices))) {
         set_error("mf_sse: bad arguments (n_slices must be in [1, %d])", kMaxSlices);
@@ -455,14 +455,33 @@ extern "C" int mf_sse(const int32_t* user_ids, const int32_t* item_ids,
         MF_HIP_CHECK(hipMemsetAsync(sse_out, 0, sizeof(double), (hipStream_t)stream));
         return MF_OK;
     }
+    if (max_blocks < 0) {
+        set_error("mf_sse_capped: max_blocks < 0");
+        return MF_ERR_INVALID;
+    }
     SseParams P{user_ids, item_ids, ratings, n_ratings, global_mean, user_biases,
                 item_biases, user_features, item_features, n_users, n_items, n_factors,
                 kernel, gamma, min_rating, max_rating, (double*)workspace, sse_out,
-                (hipStream_t)stream, S};
+                (hipStream_t)stream, S, max_blocks};
     if (dtype == MF_F32) return sse_launch_f32(P);
     if (dtype == MF_F64) return sse_launch_f64(P);
     set_error("unknown dtype code %d", dtype);
     return MF_ERR_INVALID;
+}
+
+extern "C" int mf_sse(const int32_t* user_ids, const int32_t* item_ids,
+                      const void* ratings, int64_t n_ratings,
+                      double global_mean, const void* user_biases,
+                      const void* item_biases, const void* user_features,
+                      const void* item_features, int32_t n_users, int32_t n_items,
+                      int32_t n_factors, int32_t kernel, int32_t dtype, double gamma,
+                      double min_rating, double max_rating,
+                      const int64_t* slice_offsets, int32_t n_slices, void* workspace,
+                      double* sse_out, void* stream) {
+    return mf_sse_capped(user_ids, item_ids, ratings, n_ratings, global_mean, user_biases,
+                         item_biases, user_features, item_features, n_users, n_items,
+                         n_factors, kernel, dtype, gamma, min_rating, max_rating,
+                         slice_offsets, n_slices, workspace, 0, sse_out, stream);
 }
 
 extern "C" int mf_predict(const int32_t* user_ids, const int32_t* item_ids,

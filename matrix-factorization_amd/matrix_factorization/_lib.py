@@ -71,6 +71,9 @@ SIGNATURES = {
     "mf_sse": (ctypes.c_int, [
         _P, _P, _P, _I64, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F64,
         _F64, _F64, _P, _I32, _P, _P, _P]),
+    "mf_sse_capped": (ctypes.c_int, [
+        _P, _P, _P, _I64, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _I32, _I32, _F64,
+        _F64, _F64, _P, _I32, _P, _I32, _P, _P]),
     "mf_predict": (ctypes.c_int, [
         _P, _P, _I64, _F64, _P, _P, _P, _P, _I32, _I32, _I32, _F64, _F64,
         _F64, _I32, _P, _P]),

@@ -208,9 +208,12 @@ def item_ranges(item_ids: np.ndarray, n_items: int, world: int) -> np.ndarray:
     return b
 
 
-def rotation_offset(draw: int, world: int) -> int:
-    """Item range of rank 0 in sub-epoch 0 of the epoch with this draw."""
-    return int(draw) % world
+def rotation_offset(epoch: int, world: int) -> int:
+    """Item range of rank 0 in sub-epoch 0 of epoch ``epoch``: one step back
+    per epoch, so every rank opens an epoch on the range it closed the last
+    one with (no transfer at the epoch boundary; the other ranges held
+    locally are stale until they come round the ring)."""
+    return (-int(epoch)) % world
 
 
 def rotation_range(rank: int, off: int, s: int, world: int) -> int:
@@ -232,11 +235,20 @@ class RotationExchange:
     range this rank holds is current there.  ``pass_range`` sends range
     ``c_send`` to rank - 1 and receives ``c_recv`` from rank + 1 (batched
     point-to-point: one RCCL group, two xGMI transfers per rank);
-    ``gather`` all-gathers every rank's final range at the end of an epoch.
-    With gloo and device tensors (one-GPU rehearsal) the transfers are
-    staged through host memory."""
+    ``gather`` all-gathers every rank's final range (into the live replica, or
+    into ``into``).  With gloo and device tensors (one-GPU rehearsal) the
+    transfers are staged through host memory.
 
-    def __init__(self, engine: SGDEngine, ilo: np.ndarray, group=None):
+    ``overlap``: the end-of-epoch all-gather and the training-RMSE pass leave
+    the critical path (``snapshot_sse``): the rank's P / b_u and its final
+    range are copied on the launch stream (two copies of a few MB), then, on
+    a side stream, the all-gather fills a snapshot replica and mf_sse_capped
+    computes the epoch's SSE from the snapshots with at most ``sse_blocks``
+    workgroups, beside the next epoch's sub-epochs (which use B workgroups,
+    one per CU, of the chip's CUs).  The live replica is then gathered only
+    when the caller needs it whole (``gather`` after the last epoch)."""
+
+    def __init__(self, engine: SGDEngine, ilo: np.ndarray, group=None, overlap: bool = False):
         self.e, self.group = engine, group
         self.ilo = np.asarray(ilo, np.int64)
         self.world, self.rank = world_info(group)
@@ -247,10 +259,15 @@ class RotationExchange:
                       and torch.device(dev).type == "cuda")
         self.rows = int(np.diff(self.ilo).max()) if self.world else 0
         self._gbuf = None
+        self.overlap = bool(overlap) and torch.device(dev).type == "cuda"
+        self._ov = None
+        self.sse_events = []            # (start, end) on the side stream per snapshot_sse
 
-    def _range(self, c: int):
+    def _range(self, c: int, Q=None, bi=None):
         lo, hi = int(self.ilo[c]), int(self.ilo[c + 1])
-        return self.e.Q[lo:hi], self.e.bi[lo:hi]
+        Q = self.e.Q if Q is None else Q
+        bi = self.e.bi if bi is None else bi
+        return Q[lo:hi], bi[lo:hi]
 
     def pass_range(self, c_send: int, c_recv: int) -> None:
         """Send range c_send to rank - 1, receive range c_recv from rank + 1."""
@@ -272,46 +289,119 @@ class RotationExchange:
             qr.copy_(rcv[0])
             br.copy_(rcv[1])
 
-    def gather(self, c_final: list) -> None:
-        """Every rank's final range (rank r holds c_final[r]) to every rank."""
-        if self.world == 1:
-            return
+    def _buffers(self):
         e, k, m = self.e, self.e.k, self.rows
         dev = torch.device("cpu") if self.stage else e.Q.device
         if self._gbuf is None:
             self._gbuf = (torch.zeros(m * (k + 1), dtype=e.Q.dtype, device=dev),
                           torch.empty(self.world * m * (k + 1), dtype=e.Q.dtype, device=dev))
-        mine, out = self._gbuf
-        q, b = self._range(c_final[self.rank])
+        return self._gbuf
+
+    def _pack(self, c: int) -> None:
+        """This rank's range c into the gather's send buffer (current stream)."""
+        mine, _ = self._buffers()
+        k, m = self.e.k, self.rows
+        q, b = self._range(c)
         n = q.shape[0]
         mine[: n * k].copy_(q.reshape(-1))
         mine[m * k: m * k + n].copy_(b)
+
+    def _all_gather_unpack(self, c_final: list, Q, bi, skip_own: bool) -> None:
+        mine, out = self._buffers()
+        k, m = self.e.k, self.rows
         if dist.get_backend(self.group) == "gloo":
             dist.all_gather(list(out.view(self.world, -1).unbind(0)), mine, group=self.group)
         else:
             dist.all_gather_into_tensor(out, mine, group=self.group)
         parts = out.view(self.world, m * (k + 1))
         for r in range(self.world):
-            if r == self.rank:
+            if r == self.rank and skip_own:
                 continue
-            q, b = self._range(c_final[r])
+            q, b = self._range(c_final[r], Q, bi)
             n = q.shape[0]
             q.copy_(parts[r, : n * k].view(n, k))
             b.copy_(parts[r, m * k: m * k + n])
 
+    def gather(self, c_final: list) -> None:
+        """Every rank's final range (rank r holds c_final[r]) into every rank's
+        live replica."""
+        if self.world == 1:
+            return
+        self.join()
+        self._pack(c_final[self.rank])
+        self._all_gather_unpack(c_final, None, None, skip_own=True)
+
+    def snapshot_sse(self, c_final: list, slot: int, sse_blocks: int, timing: bool = False):
+        """Epoch end in overlap mode (class docstring): snapshots on the
+        launch stream, all-gather + RMSE pass on the side stream."""
+        e = self.e
+        main = torch.cuda.current_stream(e.dev)
+        ov = self._ov
+        if ov is None:
+            ov = self._ov = dict(side=torch.cuda.Stream(e.dev), done=None,
+                                 P=torch.empty_like(e.P), bu=torch.empty_like(e.bu),
+                                 Q=torch.empty_like(e.Q), bi=torch.empty_like(e.bi),
+                                 ws=torch.empty_like(e.ws))
+        if ov["done"] is not None:
+            main.wait_event(ov["done"])          # the last pass has read the snapshots
+        ov["P"].copy_(e.P)
+        ov["bu"].copy_(e.bu)
+        own_q, own_b = self._range(c_final[self.rank])
+        snap_q, snap_b = self._range(c_final[self.rank], ov["Q"], ov["bi"])
+        snap_q.copy_(own_q)
+        snap_b.copy_(own_b)
+        if self.world > 1:
+            self._pack(c_final[self.rank])
+        ready = torch.cuda.Event()
+        ready.record(main)
+        side = ov["side"]
+        with torch.cuda.stream(side):
+            side.wait_event(ready)
+            if timing:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(side)
+            if self.world > 1:
+                self._all_gather_unpack(c_final, ov["Q"], ov["bi"], skip_own=True)
+            e.sse_from(slot, ov["P"], ov["Q"], ov["bu"], ov["bi"], ov["ws"], side, sse_blocks)
+            if timing:
+                ev[1].record(side)
+                self.sse_events.append(ev)
+        done = torch.cuda.Event()
+        done.record(side)
+        ov["done"] = done
+
+    def join(self) -> None:
+        """Make the launch stream wait for the side stream's last pass."""
+        if self._ov is not None and self._ov["done"] is not None:
+            torch.cuda.current_stream(self.e.dev).wait_event(self._ov["done"])
+
+
+def sse_blocks_beside(engine: SGDEngine, n_blocks: int) -> int:
+    """Workgroups the overlapped RMSE pass may use beside a persistent strata
+    launch of ``n_blocks`` workgroups (one per CU): the CUs left over, less a
+    margin (at least 8: one per item slice)."""
+    cus = engine._cus()
+    return max(8, cus - n_blocks - 8)
+
 
 def rotation_epoch(engine: SGDEngine, rot: RotationExchange, draw: int, lr: float, reg: float,
                    update_user: bool = True, update_item: bool = True, events=None,
-                   persistent: Optional[bool] = None, launches: Optional[list] = None) -> None:
+                   persistent: Optional[bool] = None, launches: Optional[list] = None,
+                   epoch: int = 0, sse_slot: Optional[int] = None,
+                   sse_timing: bool = False) -> None:
     """One epoch of the rotation schedule on this rank (module docstring):
-    N sub-epochs (engine.epoch_phase on the range held), N - 1 ring hand-offs,
-    one all-gather.  ``events``: a list that receives (kind, start, end)
-    timing events ("sgd" / "pass" / "gather") recorded on the launch stream.
-    ``launches``: a list that receives each sub-epoch's kernel launch count
-    (1 = persistent; synchronises after every sub-epoch)."""
+    N sub-epochs (engine.epoch_phase on the range held; offset
+    rotation_offset(epoch)), N - 1 ring hand-offs, then either the all-gather
+    into the live replica or, with ``rot.overlap`` and ``sse_slot``, the
+    snapshot + side-stream gather and RMSE pass (RotationExchange.snapshot_sse;
+    the caller then gathers the live replica once at the end).  ``events``: a
+    list that receives (kind, start, end) timing events ("sgd" / "pass" /
+    "gather") recorded on the launch stream.  ``launches``: a list that
+    receives each sub-epoch's kernel launch count (1 = persistent;
+    synchronises after every sub-epoch)."""
     world, rank = rot.world, rot.rank
     nb = engine.strata.B
-    off = rotation_offset(draw, world)
+    off = rotation_offset(epoch, world)
 
     def mark(kind, fn):
         if events is None:
@@ -333,8 +423,18 @@ def rotation_epoch(engine: SGDEngine, rot: RotationExchange, draw: int, lr: floa
             launches.append(int(out[1]))
         if s + 1 < world:
             mark("pass", lambda: rot.pass_range(c, rotation_range(rank, off, s + 1, world)))
-    mark("gather", lambda: rot.gather([rotation_range(r, off, world - 1, world)
-                                       for r in range(world)]))
+    c_final = [rotation_range(r, off, world - 1, world) for r in range(world)]
+    if rot.overlap and sse_slot is not None:
+        mark("gather", lambda: rot.snapshot_sse(c_final, sse_slot,
+                                                sse_blocks_beside(engine, nb), sse_timing))
+    else:
+        mark("gather", lambda: rot.gather(c_final))
+
+
+def rotation_final_ranges(epoch: int, world: int) -> list:
+    """The range each rank holds at the end of epoch ``epoch``."""
+    off = rotation_offset(epoch, world)
+    return [rotation_range(r, off, world - 1, world) for r in range(world)]
 
 
 class RotationReplay:
@@ -383,11 +483,11 @@ class RotationReplay:
             e.Q, e.bi = e0.Q, e0.bi
 
     def epoch(self, draw: int, lr: float, reg: float, update_user=True, update_item=True,
-              timing: bool = False, persistent: Optional[bool] = None):
-        """One rotation epoch; with ``timing`` the kernel ms of every
-        (sub-epoch, rank) as a world x world array."""
+              timing: bool = False, persistent: Optional[bool] = None, epoch: int = 0):
+        """Rotation epoch ``epoch`` (its draw ``draw``); with ``timing`` the
+        kernel ms of every (sub-epoch, rank) as a world x world array."""
         W = self.world
-        off = rotation_offset(draw, W)
+        off = rotation_offset(epoch, W)
         ms = np.zeros((W, W))
         for s in range(W):
             for rank, e in enumerate(self.engines):
@@ -399,10 +499,10 @@ class RotationReplay:
                     ms[s, rank] = t[0]
         return ms if timing else None
 
-    def serial_order(self, draw: int) -> np.ndarray:
-        """Global rating indices in the order one epoch applies them."""
+    def serial_order(self, draw: int, epoch: int = 0) -> np.ndarray:
+        """Global rating indices in the order epoch ``epoch`` applies them."""
         W = self.world
-        off = rotation_offset(draw, W)
+        off = rotation_offset(epoch, W)
         parts = []
         for s in range(W):
             for rank, e in enumerate(self.engines):
@@ -565,7 +665,8 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
         eng.load_params(Q=Q0, bi=bi0)
         ilo = item_ranges(i, n_items, world)
         eng.prepare_strata(item_bounds=ilo)
-        rot = RotationExchange(eng, ilo, group)
+        # the RMSE pass of epoch e beside epoch e+1's sub-epochs (side stream)
+        rot = RotationExchange(eng, ilo, group, overlap=True)
         nb = eng.strata.B
     else:
         ex = ReplicaExchange(eng, group)
@@ -577,6 +678,7 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
             eng.prepare_colored()
             nb = len(eng.colored) - 1
     n_total = len(u)
+    eng._ensure_sse_slots(n_epochs)       # no reallocation under a side-stream pass
     rmse = []
     draws = []
     persistent = None
@@ -587,7 +689,10 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
     def run_epoch(epoch, draw, persistent_):
         if rotate:
             rotation_epoch(eng, rot, draw, lr, reg, update_user, update_item,
-                           persistent=persistent_)
+                           persistent=persistent_, epoch=epoch,
+                           sse_slot=epoch if rot.overlap else None)
+            if rot.overlap:
+                return                        # its SSE runs on the side stream
         else:
             seq, sd = epoch_draws(np.random.RandomState([draw, rank]), nb, strata)
             if strata:
@@ -606,6 +711,8 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
                       "with the same draws as one launch per stratum", RuntimeWarning,
                       stacklevel=3)
         persistent = False
+        if rot is not None:
+            rot.join()
         eng.restore_params(snap0[0])
         if ex is not None:
             ex.flat.copy_(snap0[1])
@@ -623,11 +730,16 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
         run_epoch(epoch, draw, persistent)
         if verbose == 1:
             check(epoch + 1)
+            if rot is not None:
+                rot.join()
             rm = global_rmse(eng, epoch + 1, n_total, group)[epoch]
             rmse.append(rm)
             if rank == 0:
                 print("Epoch ", epoch + 1, "/", n_epochs, " -  train_rmse:", rm)
     check(n_epochs)
+    if rot is not None:                   # the whole replica on every rank, all SSEs in
+        rot.gather(rotation_final_ranges(n_epochs - 1, world))
+        rot.join()
     if verbose != 1:
         rmse = global_rmse(eng, n_epochs, n_total, group)
     elif persistent is False:           # a replay re-computed the printed epochs

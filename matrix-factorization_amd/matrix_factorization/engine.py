@@ -865,6 +865,23 @@ class SGDEngine:
                           0 if offs is None else len(offs) - 1, _tp(self.ws), out,
                           self.stream)
 
+    def sse_from(self, slot: int, P, Q, bu, bi, ws, stream, max_blocks: int = 0) -> None:
+        """The training SSE of the given parameter tensors (this engine's
+        ratings) into slot ``slot``, launched on ``stream`` with at most
+        ``max_blocks`` workgroups (mf_sse_capped; 0 = mf_sse's own grid).
+        ``ws``: an SSE workspace of this engine's size (not shared with a
+        concurrently running pass)."""
+        self._ensure_sse_slots(slot + 1)
+        out = _VOID(self.sse_buf.data_ptr() + 8 * slot)
+        offs = self.eval_offs
+        with torch.cuda.device(self.dev):
+            _lib.call("mf_sse_capped", _tp(self.eu), _tp(self.ei), _tp(self.er), self.n,
+                      self.global_mean, _tp(bu), _tp(bi), _tp(P), _tp(Q), self.n_users,
+                      self.n_items, self.k, self.kcode, self.dcode, self.gamma,
+                      self.min_rating, self.max_rating, _np(offs),
+                      0 if offs is None else len(offs) - 1, _tp(ws), int(max_blocks), out,
+                      _VOID(stream.cuda_stream))
+
     def sse_overlap(self, slot: int, timing: bool = False) -> None:
         """The training SSE of the current parameters into slot ``slot``,
         computed off the critical path: the parameters are copied to a device

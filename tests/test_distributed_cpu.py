@@ -418,7 +418,7 @@ def _replay(world):
     draws, sse = [], []
     for ep in range(EPOCHS):
         draws.append(int(np.random.randint(0, 2**31 - 1)))   # the fit's one draw per epoch
-        rp.epoch(draws[-1], LR, REG)
+        rp.epoch(draws[-1], LR, REG, epoch=ep)
         sse.append(rp.sse(ep))
     P, Q, bu, bi = rp.params()
     return P, Q, bu, bi, np.sqrt(np.asarray(sse) / len(u)), draws, rp
@@ -446,8 +446,8 @@ def test_rotation_epoch_is_a_sequential_sweep(world):
     P, Q, bu, bi, rmse, draws, rp = _replay(world)
     Po, Qo, buo, bio = P0.copy(), Q0.copy(), np.zeros(nu), np.zeros(ni)
     sse = []
-    for d in draws:
-        order = rp.serial_order(d)
+    for ep, d in enumerate(draws):
+        order = rp.serial_order(d, ep)
         assert np.array_equal(np.sort(order), np.arange(len(u)))     # each rating once
         oracle.sgd_pass(u, i, r, mu, buo, bio, Po, Qo, lr=LR, reg=REG, order=order)
         sse.append(oracle.sse(u, i, r, mu, buo, bio, Po, Qo))

@@ -124,7 +124,7 @@ def _gpu_replay(world, persistent=None):
     sse, draws = [], []
     for ep in range(EPOCHS):
         draws.append(int(np.random.randint(0, 2**31 - 1)))
-        rp.epoch(draws[-1], LR, REG, persistent=persistent)
+        rp.epoch(draws[-1], LR, REG, persistent=persistent, epoch=ep)
         sse.append(rp.sse(ep))
     return rp.params() + (np.sqrt(np.asarray(sse) / len(u)), rp, draws)
 
@@ -152,8 +152,8 @@ def test_kernelmf_distributed_rotate_on_one_gpu(tmp_path):
     assert np.max(np.abs(res[0]["rmse"] - rmse)) < 1e-13
     u, i, r, nu, ni, Po, Qo, mu = _mapped()
     buo, bio, sse = np.zeros(nu), np.zeros(ni), []
-    for d in draws:
-        order = rp.serial_order(d)
+    for ep, d in enumerate(draws):
+        order = rp.serial_order(d, ep)
         assert np.array_equal(np.sort(order), np.arange(len(u)))
         oracle.sgd_pass(u, i, r, mu, buo, bio, Po, Qo, lr=LR, reg=REG, order=order)
         sse.append(oracle.sse(u, i, r, mu, buo, bio, Po, Qo))
@@ -185,11 +185,11 @@ def test_rotation_replay_mid_size_matches_oracle_order(world):
         rp = RotationReplay(u, i, r, nu, ni, world, k, "linear", "float64", "cuda:0",
                             min_rating=1, max_rating=5, global_mean=mu)
         rp.load(P0, Q0, np.zeros(nu), np.zeros(ni))
-        for d in (11, 12):
-            rp.epoch(d, 0.01, 0.02, persistent=persistent)
+        for ep, d in enumerate((11, 12)):
+            rp.epoch(d, 0.01, 0.02, persistent=persistent, epoch=ep)
         out.append(rp.params())
         if persistent is None:
-            orders = [rp.serial_order(d) for d in (11, 12)]
+            orders = [rp.serial_order(d, ep) for ep, d in enumerate((11, 12))]
     for a, b in zip(*out):
         assert np.array_equal(a, b)
     Po, Qo, buo, bio = P0.copy(), Q0.copy(), np.zeros(nu), np.zeros(ni)

@@ -110,7 +110,7 @@ def main():
             rp.load(P0, Q0, np.zeros(nu), np.zeros(ni))
             per_ep, rmse = [], []
             for ep in range(args.epochs):
-                m = rp.epoch(bench.strata_rot(ep), args.lr, args.reg, timing=True)
+                m = rp.epoch(bench.strata_rot(ep), args.lr, args.reg, timing=True, epoch=ep)
                 sse, sms = 0.0, []
                 for e in rp.engines:
                     a, b = ev(), ev()

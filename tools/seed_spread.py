@@ -111,7 +111,7 @@ def main():
             rm = []
             for ep in range(E):
                 rp.epoch(int(np.random.RandomState([s, ep, W]).randint(0, 2**31 - 1)),
-                         args.lr, args.reg)
+                         args.lr, args.reg, epoch=ep)
                 rm.append(float(np.sqrt(rp.sse(ep) / nnz)))
             runs.append({"family": f"rotate_n{W}", "seed": s, "rmse": rm})
             log(f"rotate N={W} seed {s}: final {rm[-1]:.7f}")
