@@ -136,6 +136,11 @@ class CpuEngine:
     def sse_values(self, n):
         return self.sse_buf[:n].numpy().copy()
 
+    def _ensure_sse_slots(self, n):
+        if self.sse_buf.numel() < n:
+            self.sse_buf = torch.cat([self.sse_buf, torch.zeros(n - self.sse_buf.numel(),
+                                                                dtype=torch.float64)])
+
     def epoch_colored(self, seq, lr, reg, update_user=True, update_item=True, timing=False):
         order = np.concatenate([np.arange(self.colored[b], self.colored[b + 1])
                                 for b in seq]).astype(np.int64)
