@@ -614,6 +614,52 @@ def multi_checks(args, eng, rotate, world, rank, dev, u, i, r, nu, ni, k, kernel
     return out
 
 
+def _emulated_ring_cls():
+    from matrix_factorization.distributed import RotationExchange
+
+    class EmulatedRing(RotationExchange):
+        """Rank 0 of an N-rank rotation on one GPU (--emulate-rank): the ring
+        hand-off copies the range it would send into the rows it would
+        receive (a device copy of the same size), the all-gather unpacks this
+        rank's range N times (same bytes written); the sweeps, the snapshot
+        copies and the overlapped RMSE pass are the real ones."""
+
+        def __init__(self, engine, ilo, n, overlap=True):
+            import torch as _t
+            self.e, self.group = engine, None
+            self.ilo = np.asarray(ilo, np.int64)
+            self.world, self.rank = int(n), 0
+            self.stage = False
+            self.rows = int(np.diff(self.ilo).max())
+            self._gbuf = None
+            self.overlap = bool(overlap)
+            self._ov = None
+            self.sse_events = []
+            self._t = _t
+
+        def pass_range(self, c_send, c_recv):
+            qs, bs = self._range(c_send)
+            qr, br = self._range(c_recv)
+            n = min(qs.shape[0], qr.shape[0])
+            qr[:n].copy_(qs[:n])
+            br[:n].copy_(bs[:n])
+
+        def _all_gather_unpack(self, c_final, Q, bi, skip_own):
+            mine, out = self._buffers()
+            out.view(self.world, -1).copy_(mine.view(1, -1).expand(self.world, -1))
+            k, m = self.e.k, self.rows
+            parts = out.view(self.world, m * (k + 1))
+            for r in range(self.world):
+                if r == self.rank and skip_own:
+                    continue
+                q, b = self._range(c_final[r], Q, bi)
+                n = q.shape[0]
+                q.copy_(parts[r, : n * k].view(n, k))
+                b.copy_(parts[r, m * k: m * k + n])
+
+    return EmulatedRing
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -647,6 +693,12 @@ def main() -> int:
                     help="N > 1, --exchange delta: weight of the all-reduced item deltas "
                          "(default min(1/2, 2/N), distributed.default_delta_scale; "
                          "1.0 = plain gradient sum)")
+    ap.add_argument("--emulate-rank", type=int, default=0,
+                    help="one GPU, N > 1: run rank 0's share of an N-rank rotation run "
+                         "(its user shard, N sub-epochs over the N item ranges, the RMSE "
+                         "pass overlapped as in the real run); the ring hand-offs and the "
+                         "all-gather become device copies of the same sizes (stand-ins: "
+                         "no xGMI on one GPU); a per-rank timing probe, not a bench line")
     ap.add_argument("--rotate-no-overlap", action="store_true",
                     help="--exchange rotate: gather the replica and run the RMSE pass on the "
                          "launch stream after every epoch (default: on a side stream beside "
@@ -706,11 +758,15 @@ def main() -> int:
     if args.reg is None:
         args.reg = 0.02
 
-    if world > 1:
-        bounds = shard_users(u, nu, world)
-        lu, li, lr_ = local_shard(u, i, r, bounds, rank)
-        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    emu = args.emulate_rank if world == 1 else 0
+    if world > 1 or emu > 1:
+        nw, rk = (world, rank) if world > 1 else (emu, 0)
+        bounds = shard_users(u, nu, nw)
+        lu, li, lr_ = local_shard(u, i, r, bounds, rk)
+        lo, hi = int(bounds[rk]), int(bounds[rk + 1])
         P_local = P0[lo:hi]
+        if emu > 1:
+            args.cpu_sample = 0                # the CPU leg needs the whole workload
     else:
         lu, li, lr_, P_local = u, i, r, P0
     n_local = len(lu)
@@ -720,8 +776,8 @@ def main() -> int:
                     gamma=1.0 / k, min_rating=1.0, max_rating=5.0, global_mean=mu)
     t0 = time.time()
     strata = args.schedule == "strata"
-    rotate = world > 1 and strata and args.exchange == "rotate"
-    ilo = item_ranges(i, ni, world) if rotate else None
+    rotate = (world > 1 or emu > 1) and strata and args.exchange == "rotate"
+    ilo = item_ranges(i, ni, max(world, emu)) if rotate else None
     if strata:
         plan = eng.prepare_strata(n_blocks=args.blocks, waves=args.waves, item_bounds=ilo)
         nb = plan.B
@@ -750,7 +806,11 @@ def main() -> int:
     exch = (ReplicaExchange(eng, scale=args.delta_scale) if world > 1 and not rotate
             else None)
     # rotate: epoch e's gather + RMSE pass on a side stream beside epoch e+1
-    rot = RotationExchange(eng, ilo, overlap=not args.rotate_no_overlap) if rotate else None
+    if rotate and emu > 1:
+        rot = _emulated_ring_cls()(eng, ilo, emu, overlap=not args.rotate_no_overlap)
+    else:
+        rot = (RotationExchange(eng, ilo, overlap=not args.rotate_no_overlap) if rotate
+               else None)
     rot_overlap = rotate and rot.overlap
     eng._ensure_sse_slots(args.warmup + args.steps + 1)
 
@@ -894,7 +954,7 @@ def main() -> int:
                          "co-resident): the timed epochs are invalid")
     n_ep = args.warmup + args.steps
     if rot_overlap:           # the live replica whole again (for the checks), SSEs landed
-        rot.gather(rotation_final_ranges(n_ep - 1, world))
+        rot.gather(rotation_final_ranges(n_ep - 1, rot.world))
         rot.join()
     rmse = global_rmse(eng, n_ep, nnz)
     multi = None
@@ -994,7 +1054,12 @@ def main() -> int:
             "config": {"workload": desc, "n_users": nu, "n_items": ni, "nnz": nnz,
                        "n_factors": k, "kernel": kernel, "lr": args.lr, "reg": args.reg,
                        "schedule": sched_desc,
-                       "parallelism": f"user-sharded dp{world}" if world > 1 else "single GPU",
+                       "parallelism": (f"user-sharded dp{world}" if world > 1 else
+                                       f"EMULATION: rank 0 of a {emu}-rank rotation on one GPU "
+                                       f"(hand-offs as device copies); value = all {nnz} "
+                                       f"ratings / rank 0's epoch time, the N-rank job's rate "
+                                       f"if every rank took as long" if emu > 1 else
+                                       "single GPU"),
                        "exchange": (None if world == 1 else "rotate" if rotate else "delta"),
                        "item_delta_scale": None if exch is None else exch.scale,
                        "step": "one epoch: SGD sweep + training-RMSE pass" +
