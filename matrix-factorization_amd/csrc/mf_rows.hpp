@@ -58,6 +58,15 @@ __device__ __forceinline__ X buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
     else
         return __builtin_bit_cast(X, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, AUX));
 }
+// a * b + c with a, b < 2^24 (b wave-uniform) as ONE full-rate
+// v_mad_u32_u24: the compiler turns (uint32_t)a * b + c into a quarter-rate
+// v_mul_lo_u32 / v_mad_u64_u32 when b is a run-time value
+__device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t o;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(o) : "v"(a), "s"(b), "v"(c));
+    return o;
+}
+
 template <int AUX, typename X>
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t off, X v) {
     using U4 = __attribute__((ext_vector_type(4))) unsigned;

@@ -365,7 +365,7 @@ static int strata_epoch(const int32_t* user_ids, const int32_t* item_ids,
                    user_features, item_features, n_factors, kernel, gamma, lr, reg,
                    min_rating, max_rating, update_user_params ? 1 : 0,
                    update_item_params ? 1 : 0, flags, workspace, workspace_bytes, n_users,
-                   (hipStream_t)stream, kernel_ms, n_items, dq, dbi};
+                   (hipStream_t)stream, kernel_ms, n_items, dq, dbi, n_positions};
     if (dtype == MF_F32) return strata_launch_f32(P);
     if (dtype == MF_F64) return strata_launch_f64(P);
     set_error("unknown dtype code %d", dtype);

@@ -76,6 +76,7 @@ struct StrataArgs {
     int32_t upd_item;
     uint64_t p_bytes;        // bytes of P (write-through buffer stores: < 4 GiB)
     uint64_t bu_bytes;       // bytes of Bu (sc1 buffer loads of the bias slice)
+    uint32_t tri_bytes;      // bytes of each triple array (WT: buffer loads; < 4 GiB)
     T* Dq;                   // nullable: delta-out mode (persistent kernel): the epoch
     T* Dbi;                  //   leaves Q / Bi untouched and writes Dq = Q' - Q, Dbi
     Hyper<T> h;
@@ -147,6 +148,26 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
         if (c >= nst) c -= nst;
         return lpos + (int64_t)c * NS;
     };
+    // WT (the persistent kernel; its launcher guarantees n_users < 2^24 and
+    // the triple arrays and P below 4 GiB): row and triple offsets as 32-bit
+    // values from full-rate 24-bit multiply-adds, triples by buffer loads --
+    // no quarter-rate 32 / 64-bit multiplies and no 64-bit address math per
+    // step (the step is VALU-issue bound where HBM is not the limit)
+    [[maybe_unused]] const uint32_t kb = (uint32_t)k * (uint32_t)sizeof(T);
+    [[maybe_unused]] __amdgpu_buffer_rsrc_t tru, tri, trr;
+    [[maybe_unused]] uint32_t lpos_b = 0;
+    if constexpr (WT) {
+        tru = buf_rsrc(A.u, A.tri_bytes);
+        tri = buf_rsrc(A.i, A.tri_bytes);
+        trr = buf_rsrc(A.r, (uint64_t)A.tri_bytes / sizeof(int32_t) * sizeof(T));
+        lpos_b = (uint32_t)lpos;
+    }
+    auto qrow = [&](int i) __attribute__((always_inline)) -> VT* {
+        if constexpr (WT)
+            return reinterpret_cast<VT*>(reinterpret_cast<char*>(Qs) + mad_u24((uint32_t)i, kb, 0u));
+        else
+            return reinterpret_cast<VT*>(Qs + (size_t)i * k);
+    };
 
     // Pipeline state, two copies used alternately (the loop is unrolled by
     // two so no register holding an in-flight load is ever copied):
@@ -158,8 +179,18 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
     // the last step, never applied): a load behind a branch would make the
     // compiler drain the whole memory counter where its result is used.
     auto load_tri = [&](int t, Tri& o) __attribute__((always_inline)) {
-        const int64_t j = pos_of(t < nst ? t : nst - 1);
-        o.u = ld<true>(A.u + j); o.i = ld<true>(A.i + j); o.r = ld<true>(A.r + j);
+        if constexpr (WT) {
+            int tt = t < nst ? t : nst - 1;
+            int c = rot + tt;
+            if (c >= nst) c -= nst;
+            const uint32_t j = lpos_b + (uint32_t)c * (uint32_t)NS;     // < 2^30
+            o.u = buf_ld<2, int>(tru, j * 4u);                          // nt
+            o.i = buf_ld<2, int>(tri, j * 4u);
+            o.r = buf_ld<2, T>(trr, j * (uint32_t)sizeof(T));
+        } else {
+            const int64_t j = pos_of(t < nst ? t : nst - 1);
+            o.u = ld<true>(A.u + j); o.i = ld<true>(A.i + j); o.r = ld<true>(A.r + j);
+        }
     };
     // slot x of lane group g <- triple lane x*R + g; idle slots point at a
     // valid row (first user of the range, slab row 0) and never store.  Row
@@ -186,8 +217,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
                 const int vc = FULL || vi < kv ? vi : kv - 1;           // kv >= 1
                 if constexpr (WT)   // sc1: L2-served, never a stale L1 line
                     o.p[x][v] = buf_ld<16, VT>(
-                        prs, (uint32_t)(((uint32_t)o.u[x] * (uint32_t)k + (uint32_t)(vc * W)) *
-                                        sizeof(T)));
+                        prs, mad_u24((uint32_t)o.u[x], kb, (uint32_t)(vc * W * (int)sizeof(T))));
                 else
                     o.p[x][v] = ld<true>(row + vc);
             }
@@ -211,7 +241,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
 #pragma unroll
         for (int x = 0; x < S; ++x) {
             const bool fwd = uprev[x] == rwX.u[x];
-            const VT* row = reinterpret_cast<const VT*>(Qs + (size_t)rwX.i[x] * k);
+            const VT* row = qrow(rwX.i[x]);
 #pragma unroll
             for (int v = 0; v < V; ++v) {
                 const int vi = v * GS + l;
@@ -240,7 +270,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
                 if (A.upd_item && lead) Bis[rwX.i[x]] = sgd_bias<T, KERN>(bi[x], e, d, h);
             }
             VT* pw = reinterpret_cast<VT*>(A.P + (int64_t)rwX.u[x] * k);
-            VT* qw = reinterpret_cast<VT*>(Qs + (size_t)rwX.i[x] * k);
+            VT* qw = qrow(rwX.i[x]);
 #pragma unroll
             for (int v = 0; v < V; ++v) {
                 const int vi = v * GS + l;
@@ -253,8 +283,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
                     // range and the store is dropped -- one store per lane and
                     // step on every path keeps the vmcnt waits exact
                     const uint32_t off = (ok && A.upd_user)
-                        ? (uint32_t)(((uint32_t)rwX.u[x] * (uint32_t)k + (uint32_t)(vi * W)) *
-                                     sizeof(T))
+                        ? mad_u24((uint32_t)rwX.u[x], kb, (uint32_t)(vi * W * (int)sizeof(T)))
                         : kBufDrop;
                     buf_st<16>(prs, off, np);
                 } else {
@@ -285,7 +314,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
         for (int x = 0; x < S; ++x) {
             const bool f1 = uprev[x] == Ra.u[x];
             const bool f2 = !f1 && uprev2[x] == Ra.u[x];
-            const VT* row = reinterpret_cast<const VT*>(Qs + (size_t)Ra.i[x] * k);
+            const VT* row = qrow(Ra.i[x]);
 #pragma unroll
             for (int v = 0; v < V; ++v) {
                 const int vi = v * GS + l;
@@ -312,7 +341,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
                 if (A.upd_item && lead) Bis[Ra.i[x]] = sgd_bias<T, KERN>(bi[x], e, d, h);
             }
             VT* pw = reinterpret_cast<VT*>(A.P + (int64_t)Ra.u[x] * k);
-            VT* qw = reinterpret_cast<VT*>(Qs + (size_t)Ra.i[x] * k);
+            VT* qw = qrow(Ra.i[x]);
 #pragma unroll
             for (int v = 0; v < V; ++v) {
                 const int vi = v * GS + l;
@@ -323,8 +352,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
                 const bool ok = Ra.have[x] && (FULL || vi < kv);
                 if constexpr (WT) {
                     const uint32_t off = (ok && A.upd_user)
-                        ? (uint32_t)(((uint32_t)Ra.u[x] * (uint32_t)k + (uint32_t)(vi * W)) *
-                                     sizeof(T))
+                        ? mad_u24((uint32_t)Ra.u[x], kb, (uint32_t)(vi * W * (int)sizeof(T)))
                         : kBufDrop;
                     buf_st<16>(prs, off, np);
                 } else {
@@ -647,6 +675,7 @@ struct StrataParams {
     void* ws; size_t ws_bytes; int64_t n_users;
     hipStream_t stream; double* kernel_ms;
     int64_t n_items; void* dq; void* dbi;    // delta-out (nullable)
+    int64_t n_positions;                     // entries of each triple array
 };
 
 // workspace of the persistent kernel (int32): done[B] (position counters,
@@ -762,6 +791,12 @@ struct StrataRun {
         a.B = p.B; a.seed = p.seed; a.k = p.k; a.upd_user = p.uu; a.upd_item = p.ui;
         a.p_bytes = (uint64_t)p.n_users * (uint64_t)p.k * sizeof(T);
         a.bu_bytes = (uint64_t)p.n_users * sizeof(T);
+        // the persistent kernel's 32-bit offsets (strata_block, WT): user ids
+        // and k * sizeof(T) below 2^24, P and the triple arrays below 4 GiB
+        const uint64_t tri_bytes = (uint64_t)p.n_positions * std::max<uint64_t>(4, sizeof(T));
+        a.tri_bytes = (uint32_t)std::min<uint64_t>((uint64_t)p.n_positions * 4, 0xFFFFFFFFull);
+        const bool u32_ok = p.n_users < (1 << 24) && (uint64_t)p.k * sizeof(T) < (1u << 24) &&
+                            tri_bytes < (uint64_t)kBufDrop;
         a.Dq = static_cast<T*>(p.dq);
         a.Dbi = static_cast<T*>(p.dbi);
         if (p.dq && !p.dbi && KERN != MF_RBF) {
@@ -777,7 +812,7 @@ struct StrataRun {
             MF_HIP_CHECK(hipEventRecord(ev[0], p.stream));
         }
         bool persistent = false;
-        if ((p.flags & MF_FLAG_PERSISTENT) && p.ws && p.n_seq <= kStrataSeqArg &&
+        if ((p.flags & MF_FLAG_PERSISTENT) && p.ws && p.n_seq <= kStrataSeqArg && u32_ok &&
             p.ws_bytes >= strata_ws_bytes(p.B, p.n_seq) && a.p_bytes < (uint64_t)kBufDrop) {
             // (the deep pipeline exists for the 16- and 8-wave kernels)
             constexpr int kDeep = NW >= 8 ? 2 : 1;
