@@ -513,8 +513,8 @@ DRAW_SEED = 12345
 
 def strata_seq(ep: int, nb: int) -> np.ndarray:
     """Stratum (colour) order of bench epoch ``ep``."""
-    return np.random.RandomState((DRAW_SEED * 1000003 + ep) & 0x7FFFFFFF).permutation(
-        nb).astype(np.int32)
+    from matrix_factorization.engine import stratum_order
+    return stratum_order(np.random.RandomState((DRAW_SEED * 1000003 + ep) & 0x7FFFFFFF), nb)
 
 
 def strata_rot(ep: int) -> int:

@@ -58,7 +58,7 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
-from .engine import SGDEngine, _tp, balanced_bounds
+from .engine import SGDEngine, _tp, balanced_bounds, stratum_order
 
 
 def world_info(group=None) -> Tuple[int, int]:
@@ -225,7 +225,7 @@ def rotation_draws(draw: int, rank: int, c: int, nb: int):
     """Stratum order and step rotation of rank ``rank``'s sub-block with item
     range ``c`` in the epoch with ``draw`` (reproducible per sub-block)."""
     rs = np.random.RandomState([int(draw) & 0x7FFFFFFF, rank, c])
-    return rs.permutation(nb).astype(np.int32), int(rs.randint(0, 2**31 - 1))
+    return stratum_order(rs, nb), int(rs.randint(0, 2**31 - 1))
 
 
 class RotationExchange:
@@ -529,7 +529,7 @@ class RotationReplay:
 
 def epoch_draws(rs: np.random.RandomState, nb: int, strata: bool):
     """Stratum (colour) order and step rotation of one epoch."""
-    seq = rs.permutation(nb).astype(np.int32)
+    seq = stratum_order(rs, nb) if strata else rs.permutation(nb).astype(np.int32)
     rot = int(rs.randint(0, 2**31 - 1)) if strata else 0
     return seq, rot
 

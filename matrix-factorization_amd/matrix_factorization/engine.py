@@ -335,6 +335,32 @@ def choose_strata_blocks(u, i, n_users, n_items, k, dcode, max_blocks=None,
         B = int(np.ceil(B * 1.25)) + 1
 
 
+XCD_CLASSES = 8                  # gfx950: workgroups dealt round-robin over 8 XCDs
+
+
+def stratum_order(rs, nb: int, mode: Optional[str] = None) -> np.ndarray:
+    """The stratum order of one epoch, drawn from ``rs`` (a RandomState or
+    the ``np.random`` module).
+
+    random: a uniform permutation of the B strata.
+    xcd:    the strata grouped by s mod 8, the classes in random order and each
+            class's strata in random order (B a multiple of 8; else random).
+            Stratum t's user range r comes from the workgroup w' = w + s_t -
+            s_{t-1} (mod B); inside a class that difference is a multiple of 8,
+            so the hand-off stays on one XCD (workgroups are dealt round-robin
+            over the XCDs) and the rows come from its L2 -- every order is a
+            sequential order, the choice changes which one.
+    """
+    mode = mode or os.environ.get("MF_STRATA_ORDER", "random")
+    if mode == "xcd" and nb % XCD_CLASSES == 0 and nb > XCD_CLASSES:
+        cls = rs.permutation(XCD_CLASSES)
+        return np.concatenate([rs.permutation(np.arange(c, nb, XCD_CLASSES))
+                               for c in cls]).astype(np.int32)
+    if mode not in ("random", "xcd"):
+        raise ValueError(f"MF_STRATA_ORDER must be 'random' or 'xcd', got {mode!r}")
+    return rs.permutation(nb).astype(np.int32)
+
+
 def _under_rocprofiler() -> bool:
     """True inside `rocprofv3 ... -- python ...`: its dispatch interception
     (ROCm 7.x) segfaults on hipLaunchCooperativeKernel, so profiled runs
@@ -1223,7 +1249,7 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
             seq = np.random.permutation(nb).astype(np.int32)
             engine.epoch_colored(seq, lr, reg, update_user, update_item)
         else:
-            seq = np.random.permutation(nb).astype(np.int32)
+            seq = stratum_order(np.random, nb)
             seed = int(np.random.randint(0, 2**31 - 1))
             draws.append((seq, seed))
             engine.epoch_strata(seq, seed, lr, reg, update_user, update_item,

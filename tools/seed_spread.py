@@ -54,7 +54,7 @@ def main():
     import bench
     from matrix_factorization import _prep
     from matrix_factorization.distributed import RotationReplay
-    from matrix_factorization.engine import SGDEngine
+    from matrix_factorization.engine import SGDEngine, stratum_order
 
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
@@ -95,7 +95,7 @@ def main():
         pl = e.prepare_strata()
         for ep in range(E):
             rsd = np.random.RandomState([s, ep])
-            e.epoch_strata(rsd.permutation(pl.B).astype(np.int32),
+            e.epoch_strata(stratum_order(rsd, pl.B),
                            int(rsd.randint(0, 2**31 - 1)), args.lr, args.reg)
             e.sse_async(ep)
         rm = e.rmse_values(E)

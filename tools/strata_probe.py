@@ -20,7 +20,7 @@ import torch
 
 import bench
 from matrix_factorization import _lib
-from matrix_factorization.engine import SGDEngine
+from matrix_factorization.engine import SGDEngine, stratum_order
 
 
 def main():
@@ -55,14 +55,14 @@ def main():
             eng.epoch_strata(seq, seed, 0.01, 0.02)
 
     for ep in range(2):
-        run(rs.permutation(B).astype(np.int32), ep)
+        run(stratum_order(rs, B), ep)
     torch.cuda.synchronize()
     probe = torch.zeros(4 * B * B, dtype=torch.int64, device="cuda:0")
     _lib.call("mf_strata_set_probe", ctypes.c_void_p(probe.data_ptr()))
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
     t0.record()
-    run(rs.permutation(B).astype(np.int32), 7)
+    run(stratum_order(rs, B), 7)
     t1.record()
     torch.cuda.synchronize()
     _lib.call("mf_strata_set_probe", None)
