@@ -330,13 +330,14 @@ def run_topk(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
     scores = n_query * ni * args.steps
     ts = 4 if args.dtype == "float32" else 8
     achieved = scores * k * ts / elapsed / 1e9
-    path = ("MFMA filter (k_topk_mm + k_topk_mm_merge, exact rescoring)" if mm else
+    mmk = "k_topk_mw" if amount <= 16 and os.environ.get("MF_TOPK_MW") != "0" else "k_topk_mm"
+    path = (f"MFMA filter ({mmk} + k_topk_mm_merge, exact rescoring)" if mm else
             "two-stage (keys in HBM)" if os.environ.get("MF_TOPK_TWO_STAGE") == "1"
             else "fused (k_topk_fused + k_topk_merge)")
     if mm:
         tf = scores * 2 * k / elapsed / 1e12
         roof = {"bound": "mfma", "achieved": tf, "peak": 157.3, "unit": "TFLOP/s",
-                "frac": tf / 157.3, "traffic": None, "kernel": "k_topk_mm",
+                "frac": tf / 157.3, "traffic": None, "kernel": mmk,
                 "note": "2k flops per score on v_mfma_f32_32x32x2_f32 (f32 MFMA peak); device "
                         "time of the mf_topk_mm launches (inputs resident) incl. the merge"}
     else:

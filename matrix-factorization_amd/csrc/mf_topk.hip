@@ -574,25 +574,31 @@ __device__ __forceinline__ void mm_sort(float* sc, int32_t* id, int n, int t) {
     }
 }
 
-// One wave sorts a 256-entry list in LDS by (score desc, id asc): bitonic,
-// two compare-exchange pairs per lane and stage, no workgroup barrier (LDS
-// operations of one wave complete in order; the empty asm keeps the compiler
-// from moving a lane's accesses across stages, i.e. from forwarding its own
-// stores where another lane wrote).
-__device__ __forceinline__ void wave_sort256(float* sc, int32_t* id, int lane) {
-    for (int sz = 2; sz <= kMmCap; sz <<= 1) {
+// One wave sorts an N-entry list (N a power of two, 64 <= N <= 256) in LDS
+// by (score desc, id asc): bitonic, N / 128 compare-exchange pairs per lane
+// and stage (N = 64: lanes 0..31), no workgroup barrier (LDS operations of
+// one wave complete in order; the empty asm keeps the compiler from moving a
+// lane's accesses across stages, i.e. from forwarding its own stores where
+// another lane wrote).
+template <int N = kMmCap>
+__device__ __forceinline__ void wave_sort(float* sc, int32_t* id, int lane) {
+    static_assert(N >= 64 && N <= 256 && (N & (N - 1)) == 0, "64..256, a power of two");
+    constexpr int E = N >= 128 ? N / 128 : 1;
+    for (int sz = 2; sz <= N; sz <<= 1) {
         for (int st = sz >> 1; st > 0; st >>= 1) {
 #pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int pi = lane + 64 * e;                 // pair index 0..127
-                const int x = (pi / st) * 2 * st + (pi % st), y = x + st;
-                const bool desc = (x & sz) == 0;
-                const float kx = sc[x], ky = sc[y];
-                const int32_t ix = id[x], iy = id[y];
-                const bool xfirst = kx > ky || (kx == ky && ix < iy);
-                if (desc ? !xfirst : xfirst) {
-                    sc[x] = ky; sc[y] = kx;
-                    id[x] = iy; id[y] = ix;
+            for (int e = 0; e < E; ++e) {
+                const int pi = lane + 64 * e;                 // pair index 0..N/2-1
+                if (N >= 128 || pi < N / 2) {
+                    const int x = (pi / st) * 2 * st + (pi % st), y = x + st;
+                    const bool desc = (x & sz) == 0;
+                    const float kx = sc[x], ky = sc[y];
+                    const int32_t ix = id[x], iy = id[y];
+                    const bool xfirst = kx > ky || (kx == ky && ix < iy);
+                    if (desc ? !xfirst : xfirst) {
+                        sc[x] = ky; sc[y] = kx;
+                        id[x] = iy; id[y] = ix;
+                    }
                 }
             }
             asm volatile("" ::: "memory");
@@ -607,31 +613,52 @@ __device__ __forceinline__ void wave_sort256(float* sc, int32_t* id, int lane) {
 // at most `extra` excluded ids in the range) tau is the (amount + extra)-th
 // best, of which at least `amount` are not excluded.  Returns the band
 // size; *adm receives the admission bound.
+template <int CAP = kMmCap>
 __device__ __forceinline__ int wave_compact(const MmArgs& A, float* sc, int32_t* id, int n,
                                             bool check, int64_t elo, int64_t ehi, int extra,
                                             float mg, int lane, float* adm) {
-    for (int y = lane; y < kMmCap; y += kWave) {
+    if constexpr (CAP == kWave) {
+        // one entry per lane: the excluded ids of the range come in 64 at a
+        // time (one parallel load instead of a chain of dependent binary-
+        // search loads per entry) and every lane compares its id with each
         float v = -INFINITY;
         int32_t it = 0x7fffffff;
-        if (y < n) {
-            v = sc[y];
-            it = id[y];
-            if (check && in_sorted(A.ex_items, elo, ehi, it)) { v = -INFINITY; it = 0x7fffffff; }
+        if (lane < n) { v = sc[lane]; it = id[lane]; }
+        bool ex = false;
+        if (check) {
+            for (int64_t b0 = elo; b0 < ehi; b0 += kWave) {          // wave-uniform
+                const int64_t j = b0 + lane;
+                const int32_t e = j < ehi ? A.ex_items[j] : -1;
+                const int ne = (int)min((int64_t)kWave, ehi - b0);
+                for (int x = 0; x < ne; ++x) ex |= __builtin_amdgcn_readlane(e, x) == it;
+            }
         }
-        sc[y] = v;
-        id[y] = it;
+        sc[lane] = ex ? -INFINITY : v;
+        id[lane] = ex ? 0x7fffffff : it;
+    } else {
+        for (int y = lane; y < CAP; y += kWave) {
+            float v = -INFINITY;
+            int32_t it = 0x7fffffff;
+            if (y < n) {
+                v = sc[y];
+                it = id[y];
+                if (check && in_sorted(A.ex_items, elo, ehi, it)) { v = -INFINITY; it = 0x7fffffff; }
+            }
+            sc[y] = v;
+            id[y] = it;
+        }
     }
     asm volatile("" ::: "memory");
-    wave_sort256(sc, id, lane);
-    const int rank = A.amount + (check ? 0 : extra);     // <= kMmCap (caller)
+    wave_sort<CAP>(sc, id, lane);
+    const int rank = A.amount + (check ? 0 : extra);     // <= CAP (caller)
     int valid = 0, keep = 0;
     float bound = -INFINITY;
 #pragma unroll
-    for (int e = 0; e < kMmCap / kWave; ++e)
+    for (int e = 0; e < CAP / kWave; ++e)
         valid += __popcll(__ballot(sc[lane + 64 * e] != -INFINITY));
     if (valid >= rank) bound = sc[rank - 1] - 2.f * mg;
 #pragma unroll
-    for (int e = 0; e < kMmCap / kWave; ++e)
+    for (int e = 0; e < CAP / kWave; ++e)
         keep += __popcll(__ballot(sc[lane + 64 * e] != -INFINITY && sc[lane + 64 * e] >= bound));
     *adm = bound;
     return keep;
@@ -886,6 +913,349 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
     if (tid == 0 && s_lost) atomicOr(A.overflow, 1);
 }
 
+// k_topk_mw (round 3; amount <= kMwMaxAmount): k_topk_mm's filter with the
+// users spread over the waves instead of the items.  Each of the four waves
+// owns 32 users (one 32-row MFMA tile, A operands in registers) and a
+// wave-private LDS list of kMwCap candidates per user; all four walk the
+// same 32-item tiles of the split, so a tile's B operands come from L2 once
+// per workgroup (128 users) and the other three waves find them in the CU's
+// L1.  Nothing is shared between waves after the setup: no workgroup
+// barrier per chunk.  The list bookkeeping lives in registers -- lane r < 32
+// holds the count and the admission bound of user r of its wave -- so an
+// admitted score is written at base + (its rank among the tile's admitted
+// lanes of that user), no LDS atomics; a list that might not take another
+// tile (count > kMwCap - 32) is compacted in registers (one entry per lane:
+// exclusion check against the user's excluded ids of the split, loaded 64 at
+// a time; the amount-th best by a rank count; the band kept in lane order).
+// Admission rule, margin, exclusions and the (unsorted) bands written per
+// (user, split) are k_topk_mm's; k_topk_mm_merge sorts and rescores.
+constexpr int kMwCap = kWave;            // one entry per lane in a compaction
+constexpr int kMwMaxAmount = 16;         // amount + band must fit kMwCap - 32 after a compaction
+constexpr int kMwUsers = 32 * kWavesPerBlock;
+constexpr int kMwExCap = 768;            // excluded ids of a wave's users in its split, cached in LDS
+
+// v[l] = x (x and l wave-uniform), the other lanes keep v
+__device__ __forceinline__ int writelane_i(int x, int l, int v) {
+    return (int)(threadIdx.x & (kWave - 1)) == l ? x : v;
+}
+__device__ __forceinline__ float readlane_f(float v, int j) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j));
+}
+
+template <int SEG, bool PIPE = true>
+__global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
+    constexpr int CAP = kMwCap;
+    using f32x16 = __attribute__((ext_vector_type(16))) float;
+    __shared__ float s_sc[kMwUsers][CAP];
+    __shared__ int32_t s_id[kMwUsers][CAP];
+    __shared__ float s_m[kMwUsers];
+    __shared__ int64_t s_elo[kMwUsers], s_ehi[kMwUsers];
+    __shared__ int32_t s_ex[kWavesPerBlock][kMwExCap];   // per wave: its users' ids, packed
+    __shared__ int s_exoff[kMwUsers];                      // offset in s_ex[wave], -1: not cached
+    __shared__ int s_lost;
+    const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
+    const int c = lane & 31, h = lane >> 5;
+    const int split = blockIdx.x;
+    const int m0 = 32 * wv;                              // this wave's users: m0 .. m0 + 31
+    const int q0 = blockIdx.y * kMwUsers + m0;
+    const int k = A.k;
+    const int64_t span = ((int64_t)A.n_items + A.n_splits - 1) / A.n_splits;
+    const int ibeg = (int)min((int64_t)A.n_items, span * split);
+    const int iend = (int)min((int64_t)A.n_items, span * (split + 1));
+    const float qmax = A.stats[0], bimax = A.stats[1];
+    const float ck = 2.f * (float)(k + 8) * 0x1p-24f;
+    if (tid == 0) s_lost = 0;
+    float bu_own = 0.f;
+    int ex_n = 0;                                        // lane r < 32: excluded ids of user r in the split
+    // lane r < 32: count and admission bound of user m0 + r (no query: never admits)
+    int lcnt = 0;
+    float ladm = q0 + c < A.nq ? -INFINITY : INFINITY;
+    if (lane < 32) {
+        const int qy = q0 + lane;
+        const int32_t uu = qy < A.nq ? A.users[qy] : -1;
+        float pn = 0.f;
+        if (uu >= 0)
+            for (int f = 0; f < k; ++f) pn = __builtin_fmaf(A.P[(int64_t)uu * k + f],
+                                                            A.P[(int64_t)uu * k + f], pn);
+        pn = sqrtf(pn) * 1.0001f;
+        bu_own = uu >= 0 ? A.Bu[uu] : 0.f;
+        const float mg = ck * pn * qmax +
+                         0x1p-21f * (fabsf(A.mu) + fabsf(bu_own) + bimax + pn * qmax);
+        s_m[m0 + lane] = mg;
+        if (split == 0 && qy < A.nq) A.marg[qy] = mg;
+        int64_t lo = 0, hi = 0;
+        if (A.ex_ptr && qy < A.nq) {
+            lo = lower_pos(A.ex_items, A.ex_ptr[qy], A.ex_ptr[qy + 1], ibeg);
+            hi = lower_pos(A.ex_items, lo, A.ex_ptr[qy + 1], iend);
+        }
+        s_elo[m0 + lane] = lo;
+        s_ehi[m0 + lane] = hi;
+        ex_n = (int)(hi - lo);
+    }
+    // The excluded ids of this wave's users in the split, packed into the
+    // wave's LDS area (users in order while they fit; the rest search HBM):
+    // a compaction then checks its list without a global-memory round trip.
+    {
+        int incl = ex_n;                                 // inclusive scan over lanes 0..31
+        for (int o = 1; o < 32; o <<= 1) {
+            const int t = __shfl_up(incl, o, kWave);
+            if (c >= o) incl += t;
+        }
+        const int off = incl - ex_n;
+        const bool fits = incl <= kMwExCap;
+        if (lane < 32) s_exoff[m0 + lane] = fits ? off : -1;
+        const uint64_t fm = __builtin_amdgcn_ballot_w64(lane < 32 && fits);
+        const int nfit = __popcll(fm);                   // users 0 .. nfit-1 are cached
+        const int ntot = nfit > 0 ? __builtin_amdgcn_readlane(incl, nfit - 1) : 0;
+        asm volatile("" ::: "memory");
+        // all loads in flight first, then the LDS stores
+        constexpr int kSteps = kMwExCap / kWave;
+        int32_t val[kSteps];
+#pragma unroll
+        for (int j = 0; j < kSteps; ++j) {
+            const int t = lane + kWave * j;
+            val[j] = 0;
+            if (t < ntot) {
+                int u = 0;                               // last user whose range starts at or before t
+                for (int r = 1; r < nfit; ++r) u += __builtin_amdgcn_readlane(off, r) <= t ? 1 : 0;
+                val[j] = A.ex_items[s_elo[m0 + u] + (t - s_exoff[m0 + u])];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kSteps; ++j)
+            if (lane + kWave * j < ntot) s_ex[wv][lane + kWave * j] = val[j];
+    }
+    // A operands: lane (c, h) holds user q0 + c, columns h SEG .. h SEG + SEG-1
+    float a[SEG];
+    {
+        const int qy = q0 + c;
+        const int32_t uu = qy < A.nq ? A.users[qy] : -1;
+        const float* pr = A.P + (int64_t)(uu >= 0 ? uu : 0) * k;
+#pragma unroll
+        for (int j = 0; j < SEG; j += 4) {
+            const int c0 = h * SEG + j;
+            const float4 v = *reinterpret_cast<const float4*>(pr + (c0 < k ? c0 : 0));
+            const bool ok = uu >= 0 && c0 < k;
+            a[j + 0] = ok ? v.x : 0.f; a[j + 1] = ok ? v.y : 0.f;
+            a[j + 2] = ok ? v.z : 0.f; a[j + 3] = ok ? v.w : 0.f;
+        }
+    }
+    // accumulator row i of lane (c, h) is user r(i, h) = (i & 3) + 8 (i >> 2) + 4 h
+    float ubu[16], uadm[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int r = (i & 3) + 8 * (i >> 2) + 4 * h;
+        ubu[i] = __shfl(bu_own, r, kWave);
+        // probe (MF_TOPK_MM_DEFER=2, timing only: wrong results): admit nothing
+        uadm[i] = q0 + r < A.nq && A.defer != 2 ? -INFINITY : INFINITY;
+    }
+    __syncthreads();                                     // the setup's LDS words
+    auto load_b = [&](int it0, float (&b)[SEG], float& bi) __attribute__((always_inline)) {
+        const int n = it0 + c;
+        const int nn = n < iend ? n : ibeg;
+        const float* qr = A.Q + (int64_t)nn * k;
+        bi = A.Bi[nn];
+#pragma unroll
+        for (int j = 0; j < SEG; j += 4) {
+            const int c0 = h * SEG + j;
+            const float4 v = *reinterpret_cast<const float4*>(qr + (c0 < k ? c0 : 0));
+            b[j + 0] = v.x; b[j + 1] = v.y; b[j + 2] = v.z; b[j + 3] = v.w;
+        }
+    };
+    float b[SEG], bi;
+    load_b(ibeg, b, bi);
+    auto tile = [&](f32x16& x) __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < SEG; ++s)
+            x = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], x, 0, 0, 0);
+    };
+    // the per-row admission ballots of a tile (row i: users r(i, 0) in the
+    // low half, r(i, 1) in the high half), kept for insert
+    auto admit = [&](int c0, const f32x16& acc, float bic, uint64_t (&bal)[16])
+                     __attribute__((always_inline)) -> uint64_t {
+        const bool have = c0 + c < iend;
+        uint64_t any = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const float sp = ((A.mu + bic) + ubu[i]) + acc[i];
+            bal[i] = __builtin_amdgcn_ballot_w64(have && sp >= uadm[i]);
+            any |= bal[i];
+        }
+        return any;
+    };
+    // Compaction of user r's list (r wave-uniform): entries in lanes, excluded
+    // ones dropped (check), tau = the rank-th best (rank = amount, or amount +
+    // the split's excluded-id count where they were not checked), the band
+    // s' >= tau - 2M kept in lane order.  Returns the band's mask and sets
+    // the entries' values; the caller writes them where they belong.
+    auto compact = [&](int r, bool final_, float& v, int32_t& it, float& bound)
+                       __attribute__((always_inline)) -> uint64_t {
+        const int m = m0 + r;
+        const int n = min(__builtin_amdgcn_readlane(lcnt, r), CAP);
+        v = -INFINITY;
+        it = 0x7fffffff;
+        if (lane < n) { v = s_sc[m][lane]; it = s_id[m][lane]; }
+        const int64_t elo = s_elo[m], ehi = s_ehi[m];
+        const int extra = (int)(ehi - elo);
+        const bool check = final_ || !A.defer || A.amount + extra > (CAP - 32) / 2;
+        if (check) {
+            bool ex = false;
+            const int exo = s_exoff[m];
+            if (exo >= 0) {                              // cached in LDS
+                for (int b0 = 0; b0 < extra; b0 += kWave) {          // wave-uniform
+                    const int e = b0 + lane < extra ? s_ex[wv][exo + b0 + lane] : -1;
+                    const int ne = min(kWave, extra - b0);
+                    for (int x = 0; x < ne; ++x) ex |= __builtin_amdgcn_readlane(e, x) == it;
+                }
+            } else {
+                for (int64_t b0 = elo; b0 < ehi; b0 += kWave) {      // wave-uniform
+                    const int64_t j = b0 + lane;
+                    const int32_t e = j < ehi ? A.ex_items[j] : -1;
+                    const int ne = (int)min((int64_t)kWave, ehi - b0);
+                    for (int x = 0; x < ne; ++x) ex |= __builtin_amdgcn_readlane(e, x) == it;
+                }
+            }
+            if (ex) { v = -INFINITY; it = 0x7fffffff; }
+        }
+        // rank in (s' desc, id asc) among the entries
+        int rk = 0;
+        for (int j = 0; j < n; ++j) {
+            const float vj = readlane_f(v, j);
+            const int32_t ij = __builtin_amdgcn_readlane(it, j);
+            rk += (vj > v || (vj == v && ij < it)) ? 1 : 0;
+        }
+        const bool val = v != -INFINITY;
+        const int rank = A.amount + (check ? 0 : extra);     // <= CAP - 32 (kMwMaxAmount)
+        bound = -INFINITY;
+        if (__popcll(__builtin_amdgcn_ballot_w64(val)) >= rank) {
+            const uint64_t at = __builtin_amdgcn_ballot_w64(val && rk == rank - 1);
+            bound = readlane_f(v, (int)__builtin_ctzll(at)) - 2.f * s_m[m];
+        }
+        return __builtin_amdgcn_ballot_w64(val && v >= bound);
+    };
+    auto pos_in = [&](uint64_t mask) __attribute__((always_inline)) -> int {
+        return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                              __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+    };
+    auto insert = [&](int c0, const f32x16& acc, float bic, const uint64_t (&bal)[16])
+                      __attribute__((always_inline)) {
+        const uint32_t below = (1u << c) - 1u;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            if (bal[i]) {                                // wave-uniform
+                const int r0 = (i & 3) + 8 * (i >> 2), r1 = r0 + 4;
+                const uint32_t lo = (uint32_t)bal[i], hi = (uint32_t)(bal[i] >> 32);
+                const int base0 = __builtin_amdgcn_readlane(lcnt, r0);
+                const int base1 = __builtin_amdgcn_readlane(lcnt, r1);
+                const uint32_t half = h ? hi : lo;
+                if ((half >> c) & 1) {
+                    const int pos = (h ? base1 : base0) + __builtin_popcount(half & below);
+                    const int m = m0 + (h ? r1 : r0);
+                    if (pos < CAP) {
+                        s_sc[m][pos] = ((A.mu + bic) + ubu[i]) + acc[i];
+                        s_id[m][pos] = c0 + c;
+                    } else {
+                        s_lost = 1;
+                    }
+                }
+                lcnt = writelane_i(base0 + __builtin_popcount(lo), r0, lcnt);
+                lcnt = writelane_i(base1 + __builtin_popcount(hi), r1, lcnt);
+            }
+        }
+        // compact the lists that might not take another tile
+        uint64_t full = __builtin_amdgcn_ballot_w64(lane < 32 && lcnt > CAP - 32);
+        if (full) {
+            asm volatile("" ::: "memory");
+            while (full) {
+                const int r = __builtin_ctzll(full);          // wave-uniform
+                full &= full - 1;
+                float v, bound;
+                int32_t it;
+                const uint64_t keep = compact(r, false, v, it, bound);
+                int nk = __popcll(keep);
+                const int p = pos_in(keep);
+                if ((keep >> lane) & 1) {
+                    if (p < CAP - 32) {
+                        s_sc[m0 + r][p] = v;
+                        s_id[m0 + r][p] = it;
+                    }
+                }
+                if (nk > CAP - 32) {                          // the band does not fit
+                    if (lane == 0) s_lost = 1;
+                    nk = CAP - 32;
+                }
+                lcnt = writelane_i(nk, r, lcnt);
+                ladm = __builtin_bit_cast(float, writelane_i(__builtin_bit_cast(int, bound), r,
+                                                            __builtin_bit_cast(int, ladm)));
+                asm volatile("" ::: "memory");
+            }
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int r0 = (i & 3) + 8 * (i >> 2);
+                const float a0 = readlane_f(ladm, r0), a1 = readlane_f(ladm, r0 + 4);
+                uadm[i] = h ? a1 : a0;
+            }
+        }
+    };
+    if constexpr (PIPE) {
+        // the MFMAs of tile c+1 are issued before tile c's admission
+        f32x16 xa, xb;
+        float ba, bb;
+        tile(xa);
+        ba = bi;
+        load_b(ibeg + 32, b, bi);
+        auto step = [&](int c0, f32x16& x, float& bx, f32x16& y, float& by)
+                        __attribute__((always_inline)) {
+            tile(y);                                     // tile c+1
+            by = bi;
+            load_b(c0 + 64, b, bi);                      // tile c+2 (clamped past the range)
+            uint64_t bal[16];
+            const uint64_t any = admit(c0, x, bx, bal);
+#pragma unroll
+            for (int s = 0; s < SEG; ++s) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            }
+            if (any) insert(c0, x, bx, bal);
+        };
+        for (int c0 = ibeg; c0 < iend; c0 += 64) {
+            step(c0, xa, ba, xb, bb);
+            if (c0 + 32 < iend) step(c0 + 32, xb, bb, xa, ba);
+        }
+    } else {
+        for (int c0 = ibeg; c0 < iend; c0 += 32) {
+            f32x16 acc;
+            tile(acc);
+            const float bic = bi;
+            if (c0 + 32 < iend) load_b(c0 + 32, b, bi);
+            uint64_t bal[16];
+            if (admit(c0, acc, bic, bal)) insert(c0, acc, bic, bal);
+        }
+    }
+    // final: every list checked against the exclusions and cut to its band,
+    // written (unsorted) as this split's band of the user
+    asm volatile("" ::: "memory");
+    for (int r = 0; r < 32; ++r) {
+        const int qy = q0 + r;
+        if (qy >= A.nq) break;                           // wave-uniform
+        float v, bound;
+        int32_t it;
+        const uint64_t keep = compact(r, true, v, it, bound);
+        const int64_t o = ((int64_t)qy * A.n_splits + split) * kMmCap;
+        if ((keep >> lane) & 1) {
+            const int p = pos_in(keep);
+            A.part_s[o + p] = v;
+            A.part_id[o + p] = it;
+        }
+        if (lane == 0) A.part_n[(int64_t)qy * A.n_splits + split] = __popcll(keep);
+    }
+    __syncthreads();
+    if (tid == 0 && s_lost) atomicOr(A.overflow, 1);
+}
+
 // per user: merge the splits' bands, keep s' >= (amount-th best s') - 2M,
 // rescore those with k_read's arithmetic, rank by (score desc, id asc) --
 // the order keys and the sort of k_topk_merge, so the output is its output
@@ -993,6 +1363,29 @@ inline int topk_mm_splits(int32_t nq, int32_t n_items) {
     return (int)std::max<int64_t>(1, s);
 }
 
+// the wave-private form (k_topk_mw) for small amounts; MF_TOPK_MW=0 keeps
+// k_topk_mm (probes, A/B)
+inline bool topk_use_mw(int32_t amount) {
+    if (amount > kMwMaxAmount) return false;
+    const char* e = std::getenv("MF_TOPK_MW");
+    return !(e && std::atoi(e) == 0);
+}
+
+// k_topk_mw: 128 users per workgroup, two workgroups per CU; item splits so
+// that the grid is about one round of the resident workgroups (C3, 10K
+// users: 79 user blocks x 6 splits = 474)
+inline int topk_mw_splits(int32_t nq, int32_t n_items) {
+    if (const char* e = std::getenv("MF_TOPK_MM_SPLITS")) {      // probes
+        const int v = std::atoi(e);
+        if (v >= 1 && v <= kMmMaxSplits) return v;
+    }
+    const int64_t blocks_q = ((int64_t)nq + kMwUsers - 1) / kMwUsers;
+    int64_t s = (512 + blocks_q / 2) / blocks_q;
+    s = std::min<int64_t>(s, std::max<int64_t>(1, n_items / 2048));
+    s = std::min<int64_t>(s, kMmMaxSplits);
+    return (int)std::max<int64_t>(1, s);
+}
+
 struct TopkLaunch {
     const int32_t* users; int32_t nq; double mu; const void* bu; const void* bi;
     const void* P; const void* Q; int32_t n_items; int32_t k; double gamma, lo, hi;
@@ -1097,7 +1490,9 @@ extern "C" int32_t mf_topk_mm_supported(int32_t n_factors, int32_t kernel, int32
 
 extern "C" size_t mf_topk_mm_workspace_bytes(int32_t n_query, int32_t n_items) {
     if (n_query <= 0 || n_items <= 0) return 0;
-    const size_t ns = (size_t)topk_mm_splits(n_query, n_items);
+    // room for either kernel's bands (the launch picks by amount)
+    const size_t ns = (size_t)std::max(topk_mm_splits(n_query, n_items),
+                                       topk_mw_splits(n_query, n_items));
     return 16 + 4 * (size_t)n_query + 4 * (size_t)n_query * ns +
            8 * (size_t)n_query * ns * kMmCap;
 }
@@ -1130,7 +1525,8 @@ extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double gl
     a.P = (const float*)user_features; a.Q = (const float*)item_features;
     a.Bu = (const float*)user_biases; a.Bi = (const float*)item_biases;
     a.n_items = n_items; a.k = n_factors; a.amount = amount;
-    a.n_splits = topk_mm_splits(n_query, n_items);
+    const bool mw = topk_use_mw(amount);
+    a.n_splits = mw ? topk_mw_splits(n_query, n_items) : topk_mm_splits(n_query, n_items);
     a.mu = (float)global_mean;
     a.ex_ptr = exclude_items ? exclude_ptr : nullptr; a.ex_items = exclude_items;
     char* w = (char*)workspace;
@@ -1152,8 +1548,12 @@ extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double gl
     const dim3 grid((unsigned)a.n_splits, (unsigned)((n_query + 32 * nt - 1) / (32 * nt)));
     const char* pe = std::getenv("MF_TOPK_MM_PIPE");
     const bool pipe = pe ? std::atoi(pe) != 0 : true;
+    const dim3 grid_mw((unsigned)a.n_splits, (unsigned)((n_query + kMwUsers - 1) / kMwUsers));
 #define MF_MM_LAUNCH(S)                                                                        \
-    if (nt == 1) {                                                                            \
+    if (mw) {                                                                                 \
+        if (pipe) hipLaunchKernelGGL((k_topk_mw<S, true>), grid_mw, dim3(kBlock), 0, st, a);   \
+        else hipLaunchKernelGGL((k_topk_mw<S, false>), grid_mw, dim3(kBlock), 0, st, a);      \
+    } else if (nt == 1) {                                                                            \
         if (pipe) hipLaunchKernelGGL((k_topk_mm<S, true, 1>), grid, dim3(kBlock), 0, st, a);  \
         else hipLaunchKernelGGL((k_topk_mm<S, false, 1>), grid, dim3(kBlock), 0, st, a);      \
     } else {                                                                                  \
