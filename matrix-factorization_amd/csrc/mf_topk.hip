@@ -1139,31 +1139,29 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
         return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
                                               __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
     };
-    auto insert = [&](int c0, const f32x16& acc, float bic, const uint64_t (&bal)[16])
-                      __attribute__((always_inline)) {
+    // admitted scores of accumulator row i go to their users' lists
+    auto insert_row = [&](int i, int c0, const f32x16& acc, float bic, uint64_t bal)
+                          __attribute__((always_inline)) {
         const uint32_t below = (1u << c) - 1u;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            if (bal[i]) {                                // wave-uniform
-                const int r0 = (i & 3) + 8 * (i >> 2), r1 = r0 + 4;
-                const uint32_t lo = (uint32_t)bal[i], hi = (uint32_t)(bal[i] >> 32);
-                const int base0 = __builtin_amdgcn_readlane(lcnt, r0);
-                const int base1 = __builtin_amdgcn_readlane(lcnt, r1);
-                const uint32_t half = h ? hi : lo;
-                if ((half >> c) & 1) {
-                    const int pos = (h ? base1 : base0) + __builtin_popcount(half & below);
-                    const int m = m0 + (h ? r1 : r0);
-                    if (pos < CAP) {
-                        s_sc[m][pos] = ((A.mu + bic) + ubu[i]) + acc[i];
-                        s_id[m][pos] = c0 + c;
-                    } else {
-                        s_lost = 1;
-                    }
-                }
-                lcnt = writelane_i(base0 + __builtin_popcount(lo), r0, lcnt);
-                lcnt = writelane_i(base1 + __builtin_popcount(hi), r1, lcnt);
+        const int r0 = (i & 3) + 8 * (i >> 2), r1 = r0 + 4;
+        const uint32_t lo = (uint32_t)bal, hi = (uint32_t)(bal >> 32);
+        const int base0 = __builtin_amdgcn_readlane(lcnt, r0);
+        const int base1 = __builtin_amdgcn_readlane(lcnt, r1);
+        const uint32_t half = h ? hi : lo;
+        if ((half >> c) & 1) {
+            const int pos = (h ? base1 : base0) + __builtin_popcount(half & below);
+            const int m = m0 + (h ? r1 : r0);
+            if (pos < CAP) {
+                s_sc[m][pos] = ((A.mu + bic) + ubu[i]) + acc[i];
+                s_id[m][pos] = c0 + c;
+            } else {
+                s_lost = 1;
             }
         }
+        lcnt = writelane_i(base0 + __builtin_popcount(lo), r0, lcnt);
+        lcnt = writelane_i(base1 + __builtin_popcount(hi), r1, lcnt);
+    };
+    auto settle = [&]() __attribute__((always_inline)) {
         // compact the lists that might not take another tile
         uint64_t full = __builtin_amdgcn_ballot_w64(lane < 32 && lcnt > CAP - 32);
         if (full) {
@@ -1199,27 +1197,59 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
             }
         }
     };
+    auto insert = [&](int c0, const f32x16& acc, float bic, const uint64_t (&bal)[16])
+                      __attribute__((always_inline)) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+            if (bal[i]) insert_row(i, c0, acc, bic, bal[i]);       // wave-uniform
+        settle();
+    };
     if constexpr (PIPE) {
-        // the MFMAs of tile c+1 are issued before tile c's admission
+        // Tile c+1's MFMAs interleaved with tile c's admission, row by row:
+        // the 16 accumulator rows of tile c are compared and inserted
+        // between the SEG / 16 MFMAs of each slice of tile c+1, so the list
+        // work runs while the matrix pipe executes (an MFMA chain leaves the
+        // wave free to issue other instructions between its links).  B
+        // operands of tile c+2 are loaded in two halves, each as soon as the
+        // MFMAs of tile c+1 have read that half.
         f32x16 xa, xb;
         float ba, bb;
         tile(xa);
         ba = bi;
         load_b(ibeg + 32, b, bi);
+        auto load_half = [&](int it0, int part) __attribute__((always_inline)) {
+            const int n = it0 + c;
+            const int nn = n < iend ? n : ibeg;
+            const float* qr = A.Q + (int64_t)nn * k;
+            if (part == 0) bi = A.Bi[nn];
+            // the first part: whole float4 groups among the columns the
+            // MFMAs of slices 0..7 have read (SEG / 2 of them)
+            constexpr int H4 = (SEG / 2) & ~3;
+#pragma unroll
+            for (int j = part == 0 ? 0 : H4; j < (part == 0 ? H4 : SEG); j += 4) {
+                const int c0 = h * SEG + j;
+                const float4 v = *reinterpret_cast<const float4*>(qr + (c0 < k ? c0 : 0));
+                b[j + 0] = v.x; b[j + 1] = v.y; b[j + 2] = v.z; b[j + 3] = v.w;
+            }
+        };
         auto step = [&](int c0, f32x16& x, float& bx, f32x16& y, float& by)
                         __attribute__((always_inline)) {
-            tile(y);                                     // tile c+1
-            by = bi;
-            load_b(c0 + 64, b, bi);                      // tile c+2 (clamped past the range)
-            uint64_t bal[16];
-            const uint64_t any = admit(c0, x, bx, bal);
 #pragma unroll
-            for (int s = 0; s < SEG; ++s) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-                __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+            for (int i = 0; i < 16; ++i) y[i] = 0.f;
+            by = bi;
+            const bool have = c0 + c < iend;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+#pragma unroll
+                for (int s = i * SEG / 16; s < (i + 1) * SEG / 16; ++s)
+                    y = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], y, 0, 0, 0);
+                if (i == 7) load_half(c0 + 64, 0);       // tile c+2, columns of the first half
+                const float sp = ((A.mu + bx) + ubu[i]) + x[i];
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(have && sp >= uadm[i]);
+                if (bal) insert_row(i, c0, x, bx, bal);  // wave-uniform
             }
-            if (any) insert(c0, x, bx, bal);
+            load_half(c0 + 64, 1);
+            settle();
         };
         for (int c0 = ibeg; c0 < iend; c0 += 64) {
             step(c0, xa, ba, xb, bb);
