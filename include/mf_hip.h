@@ -65,10 +65,20 @@ enum {
     MF_FLAG_NO_COOP = 64,     /* with MF_FLAG_PERSISTENT: plain launch instead of
                                  hipLaunchCooperativeKernel (diagnostic A/B; the
                                  occupancy check is then the only guard)         */
-    MF_FLAG_NARROW = 128      /* strata: a plan built for mf_strata_slots_waves(k,
+    MF_FLAG_NARROW = 128,     /* strata: a plan built for mf_strata_slots_waves(k,
                                  dtype, 4) runs on 4-wave workgroups whose lane
                                  groups are half as wide (two vectors per lane;
                                  FP32, n_factors a multiple of 4 up to 32) */
+    MF_FLAG_L2_HANDOFF = 256  /* with MF_FLAG_PERSISTENT and an XCD-class stratum
+                                 order: a block whose user range goes next to a
+                                 workgroup on the SAME XCD (checked at run time
+                                 from the XCC ids the workgroups publish) stores
+                                 its user rows plainly, so they stay in that
+                                 XCD's L2 for the successor's loads; before a
+                                 hand-off to another XCD the producer writes its
+                                 XCD's L2 back (agent release).  Needs rows of a
+                                 whole number of 128-B lines and a 128-B aligned
+                                 P; ignored otherwise. */
 };
 
 const char* mf_last_error(void);

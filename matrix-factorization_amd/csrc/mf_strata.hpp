@@ -81,6 +81,7 @@ struct StrataArgs {
     T* Dbi;                  //   leaves Q / Bi untouched and writes Dq = Q' - Q, Dbi
     Hyper<T> h;
     int64_t* probe;          // nullable: persistent-kernel phase stamps (mf_strata_set_probe)
+    int32_t* xtab;           // nullable: MF_FLAG_L2_HANDOFF -- per workgroup (base << 4) | XCC id
 };
 
 // first step of block `blk` in this epoch (mirrored by engine.strata_mix)
@@ -124,7 +125,7 @@ template <typename T, int W, int GS, int V, int KERN, int S, bool WT = false, bo
           int DEPTH = 1, int NW = kStrataWaves>
 __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk, int ulo, int ilo,
                                              T* Qs, T* Bis, T* Bus, const Hyper<T> h,
-                                             int nus = 0) {
+                                             int nus = 0, bool keep_l2 = false) {
     using VT = typename VecOf<T, W>::type;
     constexpr int R = kWave / GS;
     constexpr int RPW = S * R;
@@ -285,7 +286,10 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
                     const uint32_t off = (ok && A.upd_user)
                         ? mad_u24((uint32_t)rwX.u[x], kb, (uint32_t)(vi * W * (int)sizeof(T)))
                         : kBufDrop;
-                    buf_st<16>(prs, off, np);
+                    // keep_l2 (wave-uniform): the successor shares this XCD's
+                    // L2 -- a plain store keeps the line there (sc1 drops it)
+                    if (keep_l2) buf_st<0>(prs, off, np);
+                    else buf_st<16>(prs, off, np);
                 } else {
                     if (ok && A.upd_user) st<true>(pw + vi, np);
                 }
@@ -354,7 +358,8 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
                     const uint32_t off = (ok && A.upd_user)
                         ? mad_u24((uint32_t)Ra.u[x], kb, (uint32_t)(vi * W * (int)sizeof(T)))
                         : kBufDrop;
-                    buf_st<16>(prs, off, np);
+                    if (keep_l2) buf_st<0>(prs, off, np);
+                    else buf_st<16>(prs, off, np);
                 } else {
                     if (ok && A.upd_user) st<true>(pw + vi, np);
                 }
@@ -587,12 +592,19 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
                                                                     int32_t* err) {
     constexpr int TH = NW * kWave;
     extern __shared__ __align__(16) unsigned char smem[];
-    __shared__ int s_abort, s_base;
+    __shared__ int s_abort, s_base, s_l2ok;
     const int B = A.B;
     const int w = blockIdx.x;
     const int ilo = A.ibnd[w], nqi = A.ibnd[w + 1] - ilo;
-    if (threadIdx.x == 0)                 // this workgroup's count at the end of the last launch
+    if (threadIdx.x == 0) {               // this workgroup's count at the end of the last launch
         s_base = __hip_atomic_load(done + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (A.xtab) {                     // publish (launch tag, XCC id)
+            unsigned v;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+            __hip_atomic_store(A.xtab + w, (s_base << 4) | (int)(v & 0xf), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
     T* Qs = reinterpret_cast<T*>(smem);
     T* Bis = Qs + (size_t)nqi * A.k;
     T* Bus = Bis + nqi;
@@ -606,6 +618,47 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
     };
     __syncthreads();
     const int base = s_base;
+    // MF_FLAG_L2_HANDOFF: once every workgroup has published its XCC id for
+    // this launch, wave 0 checks that the id depends on w mod 8 alone and that
+    // the 8 residues sit on 8 different XCDs.  With the XCD-class stratum
+    // order (checked by the launcher) a user range then moves between
+    // workgroups of ONE XCD inside a class and visits every XCD once per
+    // launch, so rows it leaves in an L2 are never read stale there.  Any
+    // doubt (a missing id after the bounded wait, another placement): off.
+    bool l2ok = false;
+    if (A.xtab) {
+        if (threadIdx.x < kWave) {
+            const int ln = threadIdx.x;
+            const int want = base << 4;
+            bool ok = true;
+            for (int64_t spins = 0;; ++spins) {          // wave-uniform
+                bool all = true;
+                for (int j = ln; j < B; j += kWave)
+                    all &= (__hip_atomic_load(A.xtab + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
+                            ~0xf) == want;
+                if (__builtin_amdgcn_ballot_w64(!all) == 0) break;
+                if (spins > kStrataSpinLimit) { ok = false; break; }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (ok) {
+                bool bad = false;
+                for (int j = ln; j < B; j += kWave)
+                    bad |= (__hip_atomic_load(A.xtab + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xf) !=
+                           (__hip_atomic_load(A.xtab + j % 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xf);
+                if (ln < 8) {
+                    const int mine = __hip_atomic_load(A.xtab + ln, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) & 0xf;
+                    for (int j = 0; j < 8; ++j)
+                        bad |= j != ln && (__hip_atomic_load(A.xtab + j, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT) & 0xf) == mine;
+                }
+                ok = __builtin_amdgcn_ballot_w64(bad) == 0;
+            }
+            if (ln == 0) s_l2ok = ok ? 1 : 0;
+        }
+        __syncthreads();
+        l2ok = s_l2ok != 0;
+    }
     for (int t = 0; t < n_seq; ++t) {
         const int s = seq.s[t];
         const int ub = (w + s) % B;
@@ -636,8 +689,12 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
         if (s_abort) return;
         stamp(t, 1);
         // the user-bias slice is staged inside the block, behind its prologue
+        // the next holder of this user range, w + s_t - s_{t+1}, on this XCD
+        // (same residue mod 8, B a multiple of 8): rows stored plainly stay
+        // in the L2 it reads; otherwise write-through, as always
+        const bool keep = l2ok && t + 1 < n_seq && ((s - seq.s[t + 1]) & 7) == 0;
         strata_block<T, W, GS, V, KERN, S, true, true, DEPTH, NW>(A, (int64_t)s * B + w, ulo, ilo, Qs,
-                                                              Bis, Bus, h, nus);
+                                                              Bis, Bus, h, nus, keep);
         __syncthreads();
         stamp(t, 2);
         if constexpr (KERN != MF_RBF) {
@@ -650,8 +707,12 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
         // signals (no L2 write-back fence: nothing handed off sits dirty in L2)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (threadIdx.x == 0)
+        if (threadIdx.x == 0) {
+            // L2 hand-offs: rows of this range stored plainly by earlier blocks
+            // on this XCD must reach memory before another XCD reads them
+            if (l2ok && !keep && t + 1 < n_seq) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             __hip_atomic_store(done + w, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         stamp(t, 3);
     }
     __syncthreads();
@@ -659,6 +720,25 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
         strata_delta_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
     else
         strata_store_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
+}
+
+// Is `seq` an XCD-class order (engine.stratum_order "xcd"): B a multiple of
+// 8 and the strata of each class s mod 8 one contiguous run, every class
+// once?  Then a user range's holder changes XCD only between runs and meets
+// each XCD in one run (MF_FLAG_L2_HANDOFF needs exactly that).
+inline bool strata_xcd_classes(const int32_t* seq, int32_t n_seq, int32_t B) {
+    if (B % 8 != 0 || B < 16 || n_seq < 1) return false;
+    bool seen[8] = {false, false, false, false, false, false, false, false};
+    int cur = -1;
+    for (int32_t t = 0; t < n_seq; ++t) {
+        const int c = ((seq[t] % 8) + 8) % 8;
+        if (c != cur) {
+            if (seen[c]) return false;
+            seen[c] = true;
+            cur = c;
+        }
+    }
+    return true;
 }
 
 // diagnostic: device buffer for the persistent kernel's phase stamps
@@ -805,6 +885,7 @@ struct StrataRun {
         }
         a.h = make_hyper<T>(p.mu, p.lr, p.reg, p.gamma, p.lo, p.hi);
         a.probe = strata_probe_ptr();
+        a.xtab = nullptr;
         hipEvent_t ev[2] = {nullptr, nullptr};
         if (p.kernel_ms) {
             MF_HIP_CHECK(hipEventCreate(&ev[0]));
@@ -825,6 +906,14 @@ struct StrataRun {
             if (persistent) {
                 int32_t* done = static_cast<int32_t*>(p.ws);
                 int32_t* err = done + p.B;
+                // the (otherwise unused) tail of the workspace holds the XCC
+                // table: rows of whole 128-B lines in a 128-B aligned P only
+                // (no line is shared by two users, so no line mixes ranges)
+                const bool lines = ((size_t)p.k * sizeof(T)) % 128 == 0 &&
+                                   (reinterpret_cast<uintptr_t>(p.P) & 127) == 0;
+                if ((p.flags & MF_FLAG_L2_HANDOFF) && lines && p.n_seq >= p.B &&
+                    strata_xcd_classes(p.seq, p.n_seq, p.B))
+                    a.xtab = err + 1;
                 int32_t nseq = p.n_seq;
                 StrataSeq sq;
                 for (int32_t t = 0; t < kStrataSeqArg; ++t) sq.s[t] = t < nseq ? p.seq[t] : 0;

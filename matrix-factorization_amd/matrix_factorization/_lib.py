@@ -24,6 +24,7 @@ MF_FLAG_PERSISTENT = 16
 MF_FLAG_DEEP_PIPE = 32
 MF_FLAG_NO_COOP = 64
 MF_FLAG_NARROW = 128
+MF_FLAG_L2_HANDOFF = 256
 MF_ERR_CAPACITY = 3
 MF_DELTA_TAKE, MF_DELTA_APPLY = 0, 1
 KERNEL_CODES = {"linear": MF_LINEAR, "sigmoid": MF_SIGMOID, "rbf": MF_RBF}

@@ -692,6 +692,11 @@ class SGDEngine:
             flags |= _lib.MF_FLAG_NO_COOP
         if pl.narrow:
             flags |= _lib.MF_FLAG_NARROW
+        # user rows handed over inside an XCD through its L2 (needs the
+        # XCD-class stratum order; the launcher checks the order, the kernel
+        # the placement) -- DESIGN.md section 5
+        if persistent and os.environ.get("MF_STRATA_L2") == "1":
+            flags |= _lib.MF_FLAG_L2_HANDOFF
         return flags
 
     def _epoch_phased(self, pl, seq, seed, lr, reg, update_user, update_item, timing,

@@ -47,3 +47,29 @@ def test_bench_two_ranks_checks_itself(exchange):
         assert m["replay"]["bit_equal"]
         assert d["phases"]["ring_pass_ms_per_epoch"] > 0
     assert d["roofline"]["frac"] > 0
+
+
+@pytest.mark.timeout(600)
+def test_bench_c4_shape_eight_ranks_rotate():
+    """configs[3] (C4) at its real shape: 1M x 100K, 100M ratings, rank 64,
+    user-sharded over 8 ranks -- here 8 gloo ranks sharing cuda:0 with
+    per-stratum launches (MF_STRATA_PERSISTENT=0: eight processes share the
+    CUs, so a persistent grid cannot count on co-residency; same bits).  The
+    line's own checks must hold at this shape: the eight replicas agree, rank
+    0's one-GPU replay of the 8-rank rotation order is bit-equal, and the
+    RMSE after 2 epochs is within 1e-3 of the N = 1 schedule's."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus",
+           "8", "--backend", "gloo", "--workload", "c3", "--steps", "1", "--warmup", "1"]
+    env = dict(os.environ, MF_STRATA_PERSISTENT="0")
+    out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=540, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["config"]["nnz"] == 100_000_000
+    assert d["config"]["exchange"] == "rotate"
+    m = d["multi_gpu"]
+    assert m["replicas_agree"] and len(set(m["replica_fingerprints"])) == 1
+    assert m["replay"]["bit_equal"]
+    assert abs(m["n1"]["rmse_gap_vs_n1"]) < 1e-3

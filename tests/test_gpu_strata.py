@@ -361,3 +361,41 @@ def test_item_phases_chosen_when_slabs_exceed_lds():
     eng2.epoch_strata(seq, 5, lr=0.01, reg=0.02, persistent=False)
     for a, b in zip(got, eng2.params_numpy()):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("kernel,k,B,waves", [("sigmoid", 32, 32, 8), ("linear", 64, 64, None),
+                                              ("linear", 32, 16, None)])
+def test_l2_handoff_equals_per_stratum_launches(kernel, k, B, waves, monkeypatch):
+    """MF_FLAG_L2_HANDOFF (MF_STRATA_L2=1 with the XCD-class stratum order):
+    inside a class the user rows are stored plainly and handed over through
+    the XCD's L2, with an L2 write-back before every hand-off to another XCD.
+    Same sequential order, so the parameters are bit-identical to one launch
+    per stratum; the kernel published every workgroup's XCC id for the
+    launch (the workspace tail), i.e. the launcher did turn it on."""
+    import torch
+
+    from matrix_factorization.engine import stratum_order
+
+    nu, ni, nnz = 4000, 2000, 300000
+    u, i, r = _synthetic(71, nu, ni, nnz)
+    rs = np.random.RandomState(72)
+    P = rs.normal(0, 0.1, (nu, k)); Q = rs.normal(0, 0.1, (ni, k))
+    bu = rs.normal(0, 0.1, nu); bi = rs.normal(0, 0.1, ni)
+    monkeypatch.setenv("MF_STRATA_L2", "1")
+    out = []
+    for persistent in (True, False):
+        eng = _engine(u, i, r, nu, ni, k, kernel, "float32", P, Q, bu, bi)
+        eng.prepare_strata(n_blocks=B, waves=waves)
+        for ep in range(3):
+            seq = stratum_order(np.random.RandomState(ep), B, "xcd")
+            eng.epoch_strata(seq, 3000 + ep, lr=0.01, reg=0.02, persistent=persistent)
+        eng.check_strata()
+        if persistent:
+            torch.cuda.synchronize()
+            ws = eng._strata_ws.cpu().numpy().view(np.int32)
+            tags = ws[B + 1: 2 * B + 1]
+            assert np.all(tags >> 4 == tags[0] >> 4) and tags[0] >> 4 > 0
+            assert len(set((tags & 0xF).tolist())) == 8
+        out.append(eng.params_numpy())
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
