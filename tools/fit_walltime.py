@@ -110,14 +110,17 @@ def main():
     eng = m._pred_engine
     same = []
     for ep in range(10):
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a, m_, b = (torch.cuda.Event(enable_timing=True) for _ in range(3))
         a.record()
         eng.epoch_strata(bench.strata_seq(ep, eng.strata.B), bench.strata_rot(ep), 0.01, 0.02)
+        m_.record()
         eng.sse_async(ep)
         b.record()
-        same.append((a, b))
+        same.append((a, m_, b))
     torch.cuda.synchronize()
-    same_ms = [a.elapsed_time(b) for a, b in same][1:]
+    same_ms = [a.elapsed_time(b) for a, _, b in same][1:]
+    same_sgd = [a.elapsed_time(m_) for a, m_, _ in same][1:]
+    same_sse = [m_.elapsed_time(b) for _, m_, b in same][1:]
     print(json.dumps({"what": "KernelMF.fit wall time", "nnz": args.nnz,
                       "n_users": m.n_users, "n_items": m.n_items, "epochs": args.epochs,
                       "prep_path": "pandas" if args.pandas_prep else "native",
@@ -135,6 +138,11 @@ def main():
                       "epoch_ms_median_2_on": float(np.median(ep_ms[1:])) if len(ep_ms) > 1
                                               else None,
                       "bench_loop_same_engine_ms_median": float(np.median(same_ms)),
+                      "bench_loop_sgd_ms_median": float(np.median(same_sgd)),
+                      "bench_loop_rmse_ms_median": float(np.median(same_sse)),
+                      "plan": {"B": int(eng.strata.B), "positions": int(eng.strata.n_positions),
+                               "max_steps": int(np.diff(eng.strata.bstep).max())
+                               if hasattr(eng.strata, "bstep") else None},
                       "bench_loop_note": ("bench.py's step (epoch_strata + sse_async) run 10x "
                                           "on fit()'s own engine and plan afterwards, epochs "
                                           "2-10"),
