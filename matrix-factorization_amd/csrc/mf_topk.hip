@@ -525,6 +525,7 @@ struct MmArgs {
     float* marg;                         // [nq]: M per user
     int32_t* overflow;
     int32_t defer;                       // light users skip the exclusion search until the end
+    int32_t fill;                        // k_topk_mw: compact a list past this many entries
 };
 
 // max item-row norm and max |b_i| (non-negative floats: integer max of the bits)
@@ -1163,7 +1164,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
     };
     auto settle = [&]() __attribute__((always_inline)) {
         // compact the lists that might not take another tile
-        uint64_t full = __builtin_amdgcn_ballot_w64(lane < 32 && lcnt > CAP - 32);
+        uint64_t full = __builtin_amdgcn_ballot_w64(lane < 32 && lcnt > A.fill);
         if (full) {
             asm volatile("" ::: "memory");
             while (full) {
@@ -1570,6 +1571,11 @@ extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double gl
     {
         const char* e = std::getenv("MF_TOPK_MM_DEFER");             // probes
         a.defer = e ? std::atoi(e) : 0;
+        // k_topk_mw: compact a list once it holds more than `fill` entries
+        // (<= kMwCap - 32: room for a whole tile).  Probes: MF_TOPK_MW_FILL.
+        const char* f = std::getenv("MF_TOPK_MW_FILL");
+        const int fv = f ? std::atoi(f) : kMwCap - 32;
+        a.fill = std::max(amount + 1, std::min(fv, kMwCap - 32));
     }
     MF_HIP_CHECK(hipMemsetAsync(stats, 0, 8, st));
     hipLaunchKernelGGL(k_topk_mm_stats, dim3((unsigned)((n_items + kBlock - 1) / kBlock)),
