@@ -33,6 +33,8 @@ def first_appearance(x, n):
 def main():
     import torch
 
+    if "--set-device" in sys.argv:         # bench.py's start: torch.cuda.set_device
+        torch.cuda.set_device(torch.device("cuda", 0))
     from matrix_factorization.engine import SGDEngine
 
     nu, ni, nnz, k = 1_000_000, 100_000, 100_000_000, 64
@@ -56,10 +58,17 @@ def main():
         lu, li, lr_ = make()
         eng = SGDEngine(lu, li, lr_, nu, ni, k, "linear", "float32", "cuda:0", gamma=1.0 / k,
                         min_rating=1.0, max_rating=5.0, global_mean=mu)
-        eng.load_params(P0, Q0, np.zeros(nu), np.zeros(ni))
-        plan = eng.prepare_strata()
+        if "--plan-first" in sys.argv:      # bench.py's order: plan, then the parameters
+            plan = eng.prepare_strata()
+            eng.load_params(P0, Q0, np.zeros(nu), np.zeros(ni))
+        else:
+            eng.load_params(P0, Q0, np.zeros(nu), np.zeros(ni))
+            plan = eng.prepare_strata()
         eng._ensure_sse_slots(8)
         ev = []
+        if "--timing-first" in sys.argv:   # bench.py's first warmup epoch: timing=True
+            eng.epoch_strata(bench.strata_seq(99, plan.B), bench.strata_rot(99), 0.01, 0.02,
+                             timing=True)
         for ep in range(7):
             a, m_, b = (torch.cuda.Event(enable_timing=True) for _ in range(3))
             a.record()
