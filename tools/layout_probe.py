@@ -31,10 +31,18 @@ def first_appearance(x, n):
 
 
 def main():
+    if "--after-bench" in sys.argv:        # bench.py's own run first, in this process
+        argv = sys.argv
+        sys.argv = ["bench.py", "--cpu-sample", "0", "--steps", "5"]
+        bench.main()
+        sys.argv = argv
     import torch
 
     if "--set-device" in sys.argv:         # bench.py's start: torch.cuda.set_device
         torch.cuda.set_device(torch.device("cuda", 0))
+    if "--warm-alloc" in sys.argv:         # one big segment in the caching allocator first
+        x = torch.empty(6 << 30, dtype=torch.uint8, device="cuda:0")
+        del x
     from matrix_factorization.engine import SGDEngine
 
     nu, ni, nnz, k = 1_000_000, 100_000, 100_000_000, 64
@@ -52,9 +60,11 @@ def main():
         "sorted": lambda: tuple(a[np.lexsort((i, u))] for a in (u, i, r)),
     }
     out = {}
-    for name, make in layouts.items():
-        if only and name not in only:
-            continue
+    names = [n for n in layouts if not only or n in only]
+    if "--twice" in sys.argv:              # the same layout twice: a second engine and plan
+        names = names + names
+    for name in names:
+        make = layouts[name]
         lu, li, lr_ = make()
         eng = SGDEngine(lu, li, lr_, nu, ni, k, "linear", "float32", "cuda:0", gamma=1.0 / k,
                         min_rating=1.0, max_rating=5.0, global_mean=mu)
@@ -65,6 +75,13 @@ def main():
             eng.load_params(P0, Q0, np.zeros(nu), np.zeros(ni))
             plan = eng.prepare_strata()
         eng._ensure_sse_slots(8)
+        arena = [a for a in sys.argv if a.startswith("--p-arena=")]
+        if arena:                          # P as a view at the start of a larger allocation
+            gb = float(arena[0].split("=")[1])
+            buf = torch.empty(int(gb * (1 << 30)) // 4, dtype=torch.float32, device="cuda:0")
+            P2 = buf[: nu * k].view(nu, k)
+            P2.copy_(eng.P)
+            eng.P = P2
         ev = []
         if "--timing-first" in sys.argv:   # bench.py's first warmup epoch: timing=True
             eng.epoch_strata(bench.strata_seq(99, plan.B), bench.strata_rot(99), 0.01, 0.02,
@@ -80,6 +97,7 @@ def main():
         torch.cuda.synchronize()
         sgd = [a.elapsed_time(m_) for a, m_, _ in ev][2:]
         sse = [m_.elapsed_time(b) for _, m_, b in ev][2:]
+        name = name if name not in out else name + "_again"
         out[name] = {"sgd_ms": float(np.median(sgd)), "rmse_ms": float(np.median(sse)),
                      "B": int(plan.B), "positions": int(plan.n_positions),
                      "max_steps": int(np.diff(plan.bstep).max())}
