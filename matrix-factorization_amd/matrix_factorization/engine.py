@@ -462,30 +462,10 @@ class SGDEngine:
         t = t.reshape(shape).contiguous()
         return t
 
-    # The user rows are read and written at random by every sweep, and how
-    # fast depends on the allocation they sit in: at C3 the sweep takes
-    # 9.4-9.6 ms with P (244 MiB) inside an allocation of >= 512 MiB and 10.1
-    # ms with P in one of 244-320 MiB (tools/layout_probe.py,
-    # profiles/r03/layout_probe_*, DESIGN.md section 5 -- most likely the
-    # translation fragment size of the segment).  So from 64 MiB up, P gets a
-    # backing buffer of ROWS_MIN_BYTES.
-    ROWS_MIN_BYTES = 1 << 30
-
-    def _dev_rows(self, a, shape) -> torch.Tensor:
-        t = self._dev(a, shape)
-        nbytes = t.numel() * t.element_size()
-        if os.environ.get("MF_ROWS_BUFFER") != "0" and (64 << 20) <= nbytes < self.ROWS_MIN_BYTES:
-            buf = torch.empty(self.ROWS_MIN_BYTES // t.element_size(), dtype=t.dtype,
-                              device=self.dev)
-            v = buf[: t.numel()].view(shape)
-            v.copy_(t)
-            t = v
-        return t
-
     def load_params(self, P=None, Q=None, bu=None, bi=None) -> None:
         """Upload parameters (NumPy or torch); None keeps the current one."""
         if P is not None:
-            self.P = self._dev_rows(P, (self.n_users, self.k))
+            self.P = self._dev(P, (self.n_users, self.k))
         if Q is not None:
             self.Q = self._dev(Q, (self.n_items, self.k))
         if bu is not None:
