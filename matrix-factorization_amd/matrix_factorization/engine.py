@@ -338,6 +338,51 @@ def choose_strata_blocks(u, i, n_users, n_items, k, dcode, max_blocks=None,
 XCD_CLASSES = 8                  # gfx950: workgroups dealt round-robin over 8 XCDs
 
 
+class _HipBlock:
+    """A physically contiguous device allocation, exposed to torch through
+    __cuda_array_interface__ (torch keeps this object alive as long as the
+    tensor's storage, and the block is freed with it)."""
+
+    _hip = None
+
+    def __init__(self, shape, dtype, dev):
+        if _HipBlock._hip is None:
+            _HipBlock._hip = ctypes.CDLL("libamdhip64.so")
+        hip = _HipBlock._hip
+        self.ptr = ctypes.c_void_p()
+        nbytes = int(np.prod(shape)) * torch.tensor([], dtype=dtype).element_size()
+        with torch.cuda.device(dev):
+            rc = hip.hipExtMallocWithFlags(ctypes.byref(self.ptr), ctypes.c_size_t(nbytes),
+                                           ctypes.c_uint(0x4))       # hipDeviceMallocContiguous
+        if rc != 0 or not self.ptr.value:
+            self.ptr = None
+            raise MemoryError(f"hipExtMallocWithFlags(contiguous, {nbytes}) failed: {rc}")
+        typestr = {torch.float32: "<f4", torch.float64: "<f8"}[dtype]
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr,
+                                         "data": (self.ptr.value, False), "version": 2,
+                                         "strides": None}
+
+    def __del__(self):
+        if getattr(self, "ptr", None) is not None and _HipBlock._hip is not None:
+            _HipBlock._hip.hipFree(self.ptr)
+            self.ptr = None
+
+
+def _contiguous_empty(shape, dtype, dev) -> Optional[torch.Tensor]:
+    """A device tensor in physically contiguous memory, or None."""
+    if dtype not in (torch.float32, torch.float64):
+        return None
+    try:
+        blk = _HipBlock(shape, dtype, dev)
+        t = torch.as_tensor(blk, device=dev)
+    except (OSError, MemoryError, RuntimeError, TypeError, KeyError):
+        return None
+    if t.data_ptr() != blk.ptr.value:            # torch copied instead of wrapping
+        return None
+    t._mf_block = blk                            # torch's storage deleter holds it too
+    return t
+
+
 def stratum_order(rs, nb: int, mode: Optional[str] = None) -> np.ndarray:
     """The stratum order of one epoch, drawn from ``rs`` (a RandomState or
     the ``np.random`` module).
@@ -462,10 +507,31 @@ class SGDEngine:
         t = t.reshape(shape).contiguous()
         return t
 
+    def _dev_rows(self, a, shape) -> torch.Tensor:
+        """P in physically contiguous device memory (hipExtMallocWithFlags,
+        hipDeviceMallocContiguous) from 16 MiB up.  Every sweep reads and
+        writes the user rows at random; measured at C3 (tools/layout_probe.py,
+        profiles/r03/layout_probe_contiguous_r03s31.json)
+        the sweep takes 9.45 ms with P contiguous and 10.1 ms when P lands in
+        memory the allocator assembled from smaller pieces (most likely the
+        address-translation fragment size), which happened in every process
+        but bench.py's.  Falls back to an ordinary allocation if the runtime
+        refuses; MF_CONTIGUOUS_ROWS=0 turns it off."""
+        t = self._dev(a, shape)
+        nbytes = t.numel() * t.element_size()
+        if (os.environ.get("MF_CONTIGUOUS_ROWS") == "0" or self.dev.type != "cuda"
+                or nbytes < (16 << 20)):
+            return t
+        v = _contiguous_empty(shape, t.dtype, self.dev)
+        if v is None:
+            return t
+        v.copy_(t)
+        return v
+
     def load_params(self, P=None, Q=None, bu=None, bi=None) -> None:
         """Upload parameters (NumPy or torch); None keeps the current one."""
         if P is not None:
-            self.P = self._dev(P, (self.n_users, self.k))
+            self.P = self._dev_rows(P, (self.n_users, self.k))
         if Q is not None:
             self.Q = self._dev(Q, (self.n_items, self.k))
         if bu is not None:

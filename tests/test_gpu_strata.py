@@ -399,3 +399,30 @@ def test_l2_handoff_equals_per_stratum_launches(kernel, k, B, waves, monkeypatch
         out.append(eng.params_numpy())
     for a, b in zip(*out):
         assert np.array_equal(a, b)
+
+
+def test_contiguous_rows_allocation():
+    """P from 16 MiB up lives in hipDeviceMallocContiguous memory wrapped by
+    torch (engine._contiguous_empty): torch's storage keeps the block alive
+    (its deleter holds a reference beside the tensor attribute), the memory
+    reads and writes as a tensor, and the engine's P uses it at C3-like size."""
+    import sys
+
+    import torch
+
+    from matrix_factorization.engine import SGDEngine, _contiguous_empty
+
+    t = _contiguous_empty((5000, 1000), torch.float32, torch.device("cuda:0"))
+    assert t is not None
+    assert sys.getrefcount(t._mf_block) >= 3       # attribute + torch's deleter + argument
+    t.fill_(3.0)
+    assert float(t.sum()) == 3.0 * 5e6
+    nu, k = 70000, 64                               # 17.9 MB of rows
+    u = np.arange(1000, dtype=np.int32) % nu
+    i = np.arange(1000, dtype=np.int32) % 50
+    eng = SGDEngine(u, i, np.ones(1000), nu, 50, k, "linear", "float32", "cuda:0",
+                    min_rating=1.0, max_rating=5.0, global_mean=1.0)
+    P = np.random.RandomState(0).normal(0, 0.1, (nu, k)).astype(np.float32)
+    eng.load_params(P, np.zeros((50, k), np.float32), np.zeros(nu), np.zeros(50))
+    assert hasattr(eng.P, "_mf_block")
+    assert np.array_equal(eng.P.cpu().numpy(), P)

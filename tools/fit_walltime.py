@@ -147,6 +147,8 @@ def main():
                                           "on fit()'s own engine and plan afterwards, epochs "
                                           "2-10"),
                       "final_train_rmse": float(m.train_rmse[-1]),
+                      "P_contiguous": hasattr(eng.P, "_mf_block"),
+                      "P_ptr": hex(eng.P.data_ptr()),
                       "synth_s": round(t_synth, 1)}))
 
 

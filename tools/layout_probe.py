@@ -75,6 +75,23 @@ def main():
             eng.load_params(P0, Q0, np.zeros(nu), np.zeros(ni))
             plan = eng.prepare_strata()
         eng._ensure_sse_slots(8)
+        if "--p-contiguous" in sys.argv:   # P in hipExtMallocWithFlags(hipDeviceMallocContiguous)
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            ptr = ctypes.c_void_p()
+            nb = nu * k * 4
+            rc = hip.hipExtMallocWithFlags(ctypes.byref(ptr), ctypes.c_size_t(nb), ctypes.c_uint(4))
+            assert rc == 0, rc
+
+            class _Buf:
+                __cuda_array_interface__ = {"shape": (nu, k), "typestr": "<f4",
+                                            "data": (ptr.value, False), "version": 2,
+                                            "strides": None}
+            P2 = torch.as_tensor(_Buf(), device="cuda:0")
+            assert P2.data_ptr() == ptr.value
+            P2.copy_(eng.P)
+            eng.P = P2
+            print("contiguous P at", hex(ptr.value), file=sys.stderr)
         arena = [a for a in sys.argv if a.startswith("--p-arena=")]
         if arena:                          # P as a view at the start of a larger allocation
             gb = float(arena[0].split("=")[1])
