@@ -401,7 +401,7 @@ class pinned_core:
 
 
 def cpu_leg(args, eng, run, serial, seq_for, rot_for, reset_params, strat_sizes, nb, strata,
-            kernel, k, mu, P0, Q0, nu, ni, n_local):
+            kernel, k, mu, P0, Q0, nu, ni, n_local, shared=None):
     """CPU baseline + parity, untimed, before the timed epochs.
 
     Full epoch (--cpu-sample -1, the default).  From the same initial state
@@ -416,6 +416,9 @@ def cpu_leg(args, eng, run, serial, seq_for, rot_for, reset_params, strat_sizes,
       (c) as (b) with another shuffle seed: the reference's own
           seed-to-seed spread at this size, the yardstick for (b).
     (b) and (c) run concurrently in two threads (ctypes drops the GIL).
+    They do not depend on the GPU's dtype (the FP64 and FP32 runs start from
+    the same FP32-representable values): computed once per bench run and kept
+    in ``shared``.
     --cpu-sample N > 0: the first strata of epoch 1 covering >= N ratings,
     (a) only."""
     import concurrent.futures as cf
@@ -474,7 +477,8 @@ def cpu_leg(args, eng, run, serial, seq_for, rot_for, reset_params, strat_sizes,
         "sgd_only": S / t_sgd, "affinity": core, **host,
     }
     parity = {
-        "what": (f"{what} from the same initial state: (a) GPU FP32 strata vs CPU oracle "
+        "what": (f"{what} from the same initial state: (a) GPU "
+                 f"{'FP32' if args.dtype == 'float32' else 'FP64'} strata vs CPU oracle "
                  f"FP64 in the GPU's serialised order"
                  + ("; (b) oracle in the reference's np.random.shuffle order; (c) the same, "
                     "another shuffle seed (the reference's own seed spread)" if full else "")),
@@ -494,9 +498,14 @@ def cpu_leg(args, eng, run, serial, seq_for, rot_for, reset_params, strat_sizes,
             np.random.RandomState(seed).shuffle(o)       # = np.random.shuffle(X), :371
             return epoch(o)[1]
 
-        log("cpu oracle (b), (c): the same epoch in two np.random.shuffle orders, 2 threads")
-        with cf.ThreadPoolExecutor(2) as ex:
-            rm_b, rm_c = ex.map(shuffled, (7, 8))
+        if shared is not None and "ref_order" in shared:
+            rm_b, rm_c = shared["ref_order"]
+        else:
+            log("cpu oracle (b), (c): the same epoch in two np.random.shuffle orders, 2 threads")
+            with cf.ThreadPoolExecutor(2) as ex:
+                rm_b, rm_c = ex.map(shuffled, (7, 8))
+            if shared is not None:
+                shared["ref_order"] = (rm_b, rm_c)
         parity.update({
             "rmse_shuffle_order": rm_b, "rmse_shuffle_order_seed2": rm_c,
             "abs_diff_strata_vs_shuffle": abs(rm_a - rm_b),
@@ -512,8 +521,9 @@ def cpu_leg(args, eng, run, serial, seq_for, rot_for, reset_params, strat_sizes,
 DRAW_SEED = 12345
 
 
-def strata_seq(ep: int, nb: int) -> np.ndarray:
-    """Stratum (colour) order of bench epoch ``ep``."""
+def strata_seq(ep: int, nb) -> np.ndarray:
+    """Stratum (colour) order of bench epoch ``ep``; ``nb`` = a strata plan
+    (its B and user-range classes) or a colour / stratum count."""
     from matrix_factorization.engine import stratum_order
     return stratum_order(np.random.RandomState((DRAW_SEED * 1000003 + ep) & 0x7FFFFFFF), nb)
 
@@ -597,7 +607,7 @@ def multi_checks(args, eng, rotate, world, rank, dev, u, i, r, nu, ni, k, kernel
         e1.load_params(P=P0, Q=Q0, bu=np.zeros(nu), bi=np.zeros(ni))
         plan1 = e1.prepare_strata()
         for ep in range(n_ep):
-            e1.epoch_strata(strata_seq(ep, plan1.B), strata_rot(ep), args.lr, args.reg)
+            e1.epoch_strata(strata_seq(ep, plan1), strata_rot(ep), args.lr, args.reg)
             e1.sse_async(ep)
         rm1 = e1.rmse_values(n_ep)
         del e1
@@ -613,6 +623,50 @@ def multi_checks(args, eng, rotate, world, rank, dev, u, i, r, nu, ni, k, kernel
             + f"RMSE gap vs N=1 {out['n1']['rmse_gap_vs_n1']:+.3e}")
     dist.barrier()
     return out
+
+
+def emulation_fields(args, out, elapsed, emu, nnz, dev, u, i, r, nu, ni, k, kernel, mu, P0,
+                     Q0) -> None:
+    """--emulate-rank: the line is a per-rank timing probe, not a rate.  The
+    measured rank-0 epoch goes to ``projection`` next to the same box's N=1
+    epoch (the single-GPU default schedule, same data, dtype and epochs);
+    ``value`` is null and ``metric`` names the probe, so no parser can take
+    the projection for a measured job rate."""
+    import torch
+
+    from matrix_factorization.engine import SGDEngine
+
+    per_rank_ms = elapsed / args.steps * 1e3
+    hyp = dict(gamma=1.0 / k, min_rating=1.0, max_rating=5.0, global_mean=mu)
+    e1 = SGDEngine(u, i, r, nu, ni, k, kernel, args.dtype, dev, **hyp)
+    e1.load_params(P=P0, Q=Q0, bu=np.zeros(nu), bi=np.zeros(ni))
+    plan1 = e1.prepare_strata()
+    n_ep = args.warmup + args.steps
+    for ep in range(args.warmup):
+        e1.epoch_strata(strata_seq(ep, plan1), strata_rot(ep), args.lr, args.reg)
+        e1.sse_async(ep)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for ep in range(args.warmup, n_ep):
+        e1.epoch_strata(strata_seq(ep, plan1), strata_rot(ep), args.lr, args.reg)
+        e1.sse_async(ep)
+    torch.cuda.synchronize(dev)
+    n1_ms = (time.perf_counter() - t0) / args.steps * 1e3
+    del e1
+    torch.cuda.empty_cache()
+    out["metric"] = f"EMULATION probe: rank 0's epoch of a {emu}-rank rotation on one GPU"
+    out["value"] = None
+    out["unit"] = None
+    out["projection"] = {
+        "per_rank_epoch_ms": per_rank_ms,
+        "n1_epoch_ms_same_box": n1_ms,
+        "projected_speedup": n1_ms / per_rank_ms,
+        "projected_job_rate": nnz / (per_rank_ms / 1e3),
+        "note": ("rank 0's share (its user shard, N sub-epochs, ring hand-offs as device "
+                 "copies of the same size) timed alone on one GPU; the N-GPU job would run "
+                 "at this rate only if every rank took as long and the xGMI hand-offs cost "
+                 "what the copies cost"),
+    }
 
 
 def _emulated_ring_cls():
@@ -667,7 +721,10 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
-    ap.add_argument("--dtype", default="float32", choices=["float32", "float64"])
+    ap.add_argument("--dtype", default="auto", choices=["auto", "float32", "float64"],
+                    help="SGD workloads: auto (default) = the reference's FP64 arithmetic "
+                         "as the headline line, the FP32 perf layout measured in the same "
+                         "run and nested as `fp32_layout`; ALS / top-k: auto = float32")
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--reg", type=float, default=None,
                     help="default 0.02 for SGD (project_template/pipeline/train.py:29-36), "
@@ -719,11 +776,6 @@ def main() -> int:
     import torch.distributed as dist
 
     from matrix_factorization import _lib
-    from matrix_factorization.distributed import (ReplicaExchange, RotationExchange,
-                                                  any_rank_failed, global_rmse, item_ranges,
-                                                  local_shard, rotation_epoch,
-                                                  rotation_final_ranges, shard_users)
-    from matrix_factorization.engine import SGDEngine, strata_slots
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -747,18 +799,69 @@ def main() -> int:
     u, i, r = synth(nu, ni, nnz)
     log(f"data: {nnz} ratings {nu}x{ni} in {time.time() - t0:.1f}s")
     mu = float(np.mean(r, dtype=np.float64))
+    # the initial state: N(0, 0.1) draws (kernel_matrix_factorization.py:97-102)
+    # rounded to FP32, so the FP64 and FP32 runs (and the CPU oracle's legs)
+    # start from exactly the same values
     rs = np.random.RandomState(7)
-    P0 = rs.normal(0.0, 0.1, (nu, k)).astype(args.dtype)
-    Q0 = rs.normal(0.0, 0.1, (ni, k)).astype(args.dtype)
-    if kernel == "als":
-        if world > 1:
-            raise SystemExit("the ALS workload (configs[4]) is a single-GPU config")
-        return run_als(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev)
-    if kernel == "topk":
+    P0 = rs.normal(0.0, 0.1, (nu, k)).astype(np.float32)
+    Q0 = rs.normal(0.0, 0.1, (ni, k)).astype(np.float32)
+    if kernel in ("als", "topk"):
+        if args.dtype == "auto":
+            args.dtype = "float32"
+        P0, Q0 = P0.astype(args.dtype), Q0.astype(args.dtype)
+        if kernel == "als":
+            if world > 1:
+                raise SystemExit("the ALS workload (configs[4]) is a single-GPU config")
+            return run_als(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev)
         return run_topk(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev)
     if args.reg is None:
         args.reg = 0.02
+    dtypes = ["float64", "float32"] if args.dtype == "auto" else [args.dtype]
+    shared = {}
+    outs = []
+    for dt in dtypes:
+        log(f"---- {dt} run")
+        outs.append(run_sgd(args, dt, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc,
+                            mu, P0, Q0, shared))
+        torch.cuda.empty_cache()
+    if rank == 0:
+        out = outs[0]
+        if len(outs) > 1:
+            out["fp32_layout"] = nested_line(outs[1])
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
 
+
+def nested_line(o: dict) -> dict:
+    """The FP32 perf-layout run, nested under the FP64 headline line."""
+    keep = ("value", "unit", "ms_per_step", "dtype", "final_rmse", "rmse_per_epoch",
+            "roofline", "phases", "parity", "multi_gpu", "projection", "schedule_build_s")
+    d = {kk: o.get(kk) for kk in keep if kk in o}
+    d["schedule"] = o["config"]["schedule"]
+    d["arithmetic"] = ("FP32 parameters; fused multiply-adds, v_exp_f32 / v_rcp_f32 "
+                       "(DESIGN.md section 3): not the reference's expression order, "
+                       "parity as a tolerance vs the FP64 oracle")
+    return d
+
+
+def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc, mu, P0, Q0,
+            shared) -> dict:
+    """One SGD bench run in ``dtype`` (float64: the reference's arithmetic,
+    float32: the perf layout).  Returns the JSON line (rank 0) or None."""
+    import torch
+    import torch.distributed as dist
+
+    from matrix_factorization.distributed import (ReplicaExchange, RotationExchange,
+                                                  any_rank_failed, global_rmse, item_ranges,
+                                                  local_shard, rotation_epoch,
+                                                  rotation_final_ranges, shard_users)
+    from matrix_factorization.engine import SGDEngine, strata_slots
+
+    args = argparse.Namespace(**{**vars(args), "dtype": dtype})
+    P0, Q0 = P0.astype(dtype), Q0.astype(dtype)
     emu = args.emulate_rank if world == 1 else 0
     if world > 1 or emu > 1:
         nw, rk = (world, rank) if world > 1 else (emu, 0)
@@ -781,15 +884,21 @@ def main() -> int:
     ilo = item_ranges(i, ni, max(world, emu)) if rotate else None
     if strata:
         plan = eng.prepare_strata(n_blocks=args.blocks, waves=args.waves, item_bounds=ilo)
-        nb = plan.B
+        nb = plan.n_strata                   # strata per epoch (C*B with C user-range classes)
+        B = plan.B                           # workgroups / item slabs
+        cls = plan.classes
         n_phases = len(getattr(plan, "phases", [plan]))   # item phases (PhasedStrata)
         strat_sizes = plan.stratum_sizes()           # ratings per stratum (launch)
         fill = n_local / max(plan.n_positions, 1)
         sched_desc = ((f"strata rotation ({n_phases} item ranges passed round the ring: "
-                       f"{n_phases} sub-epochs x B={nb} strata on this rank's sub-block, "
+                       f"{n_phases} sub-epochs x {nb} strata (B={B}"
+                       f"{f', {cls} user-range classes' if cls > 1 else ''}) on this rank's "
+                       f"sub-block, "
                        if rotate else
-                       f"strata ({n_phases} item phases x B={nb} strata, " if n_phases > 1
-                       else f"strata (B={nb}: {nb} launches/epoch, ")
+                       f"strata ({n_phases} item phases x {nb} strata of B={B}, " if n_phases > 1
+                       else f"strata (B={B}: {nb} launches/epoch, ")
+                      + (f"{cls} user-range classes ({cls * B} user ranges, {cls - 1} "
+                         f"block(s) of slack per hand-off), " if cls > 1 else "")
                       + "item slabs in LDS, "
                       f"{plan.NS} user-owned slots "
                       f"({256 if plan.narrow else plan.NS * 1024 // strata_slots(k, eng.dcode)} "
@@ -823,7 +932,7 @@ def main() -> int:
             eng.load_params(Q=Q0, bi=np.zeros(ni))
 
     def seq_for(ep):
-        return strata_seq(ep, nb)
+        return strata_seq(ep, plan if strata else nb)
 
     def rot_for(ep):          # colour-rotation seed of a strata epoch (rotate: the epoch draw)
         return strata_rot(ep)
@@ -868,7 +977,7 @@ def main() -> int:
     if world == 1 and args.cpu_sample != 0:
         cpu_baseline, parity = cpu_leg(args, eng, run, serial, seq_for, rot_for, reset_params,
                                        strat_sizes, nb, strata, kernel, k, mu, P0, Q0, nu, ni,
-                                       n_local)
+                                       n_local, shared)
 
     # ---------------- warmup + timed epochs
     reset_params()
@@ -926,7 +1035,7 @@ def main() -> int:
             persistent = n_launch == n_phases
             if persistent:           # one persistent launch per epoch (per item phase)
                 sched_desc = sched_desc.replace(
-                    f"B={nb}: {nb} launches/epoch", f"B={nb} strata in 1 persistent launch/epoch")
+                    f"B={B}: {nb} launches/epoch", f"B={B}, {nb} strata in 1 persistent launch/epoch")
                 if rotate:
                     sched_desc = sched_desc.replace("strata on this rank's sub-block",
                                                     "strata in 1 persistent launch per sub-epoch")
@@ -981,7 +1090,7 @@ def main() -> int:
             # once per stratum (per-stratum launches)
             slab_passes = 1 if persistent else nb
             alg_epoch = (plan.n_positions * (8 + ts) + n_local * 2 * k * ts
-                         + n_phases * nb * 2 * n_users_local * ts
+                         + n_phases * B * 2 * n_users_local * ts
                          + slab_passes * 2 * ni * (k + 1) * ts)
         else:
             alg_epoch = n_local * survey_per_update
@@ -1057,9 +1166,8 @@ def main() -> int:
                        "schedule": sched_desc,
                        "parallelism": (f"user-sharded dp{world}" if world > 1 else
                                        f"EMULATION: rank 0 of a {emu}-rank rotation on one GPU "
-                                       f"(hand-offs as device copies); value = all {nnz} "
-                                       f"ratings / rank 0's epoch time, the N-rank job's rate "
-                                       f"if every rank took as long" if emu > 1 else
+                                       f"(hand-offs as device copies); not a measurement of "
+                                       f"the N-GPU job: see `projection`" if emu > 1 else
                                        "single GPU"),
                        "exchange": (None if world == 1 else "rotate" if rotate else "delta"),
                        "item_delta_scale": None if exch is None else exch.scale,
@@ -1071,11 +1179,13 @@ def main() -> int:
             "cpu_baseline": cpu_baseline, "parity": parity, "multi_gpu": multi,
             "schedule_build_s": t_sched,
         }
-        print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    return 0
+        if emu > 1:
+            emulation_fields(args, out, elapsed, emu, nnz, dev, u, i, r, nu, ni, k, kernel, mu,
+                             P0, Q0)
+        return out
+    return None
+
+
 
 
 if __name__ == "__main__":

@@ -69,7 +69,7 @@ enum {
                                  dtype, 4) runs on 4-wave workgroups whose lane
                                  groups are half as wide (two vectors per lane;
                                  FP32, n_factors a multiple of 4 up to 32) */
-    MF_FLAG_L2_HANDOFF = 256  /* with MF_FLAG_PERSISTENT and an XCD-class stratum
+    MF_FLAG_L2_HANDOFF = 256, /* with MF_FLAG_PERSISTENT and an XCD-class stratum
                                  order: a block whose user range goes next to a
                                  workgroup on the SAME XCD (checked at run time
                                  from the XCC ids the workgroups publish) stores
@@ -78,8 +78,14 @@ enum {
                                  hand-off to another XCD the producer writes its
                                  XCD's L2 back (agent release).  Needs rows of a
                                  whole number of 128-B lines and a 128-B aligned
-                                 P; ignored otherwise. */
+                                 P; ignored otherwise (and with user-range
+                                 classes C > 1). */
+    /* mf_sgd_epoch_strata: bits 24..27 = C - 1, the plan's user-range classes
+       (mf_strata_plan_build_classes; 0 = C = 1, the plain B x B plan) */
+    MF_FLAG_CLASSES_SHIFT = 24
 };
+/* Largest number of user-range classes a strata plan may have. */
+#define MF_STRATA_MAX_CLASSES 4
 
 const char* mf_last_error(void);
 int mf_abi_version(void);
@@ -168,6 +174,16 @@ size_t mf_sgd_workspace_bytes(int32_t n_launch);
  * the call falls back to one launch per stratum.  The result
  * is the same sequential order either way.  kernel_ms (HOST, optional):
  * elapsed ms of the whole call and the launch count (synchronises).
+ *
+ * User-range classes (flags bits 24..27 = C - 1, a plan from
+ * mf_strata_plan_build_classes): C*B user ranges, B item ranges, C*B strata;
+ * block (s, w) = user range (s + C*w) mod C*B x item range w, so stratum s
+ * touches the user ranges of class s mod C only.  The persistent kernel
+ * then needs strata_seq to cycle through the classes (seq[t] mod C ==
+ * seq[t mod C] mod C, the first C entries of distinct classes): a user range
+ * used at position t was last used at t - C, so every hand-off has C - 1
+ * whole blocks of slack (no waiting on the chain's jitter); any other order
+ * runs as one launch per stratum.  n_seq may then be up to 1024.
  */
 int mf_sgd_epoch_strata(const int32_t* user_ids, const int32_t* item_ids,
                         const void* ratings, int64_t n_positions, int32_t n_blocks,
@@ -522,6 +538,16 @@ int mf_sched_slices(const int32_t* user_ids, const int32_t* item_ids,
  *   mf_strata_plan_free
  */
 typedef struct mf_strata_plan mf_strata_plan;
+/* The same with n_classes user-range classes: user_bounds has
+ * n_classes * n_blocks + 1 entries, block_steps (fetch) n_classes * n_blocks^2
+ * + 1; block (s, w), s < n_classes * n_blocks, = user range (s + n_classes*w)
+ * mod (n_classes * n_blocks) x item range w.  n_classes = 1 is
+ * mf_strata_plan_build. */
+int mf_strata_plan_build_classes(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
+                                 int32_t n_users, int32_t n_items, int32_t n_blocks,
+                                 int32_t n_classes, const int32_t* user_bounds,
+                                 const int32_t* item_bounds, int32_t n_slots,
+                                 mf_strata_plan** plan_out);
 int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
                          int32_t n_users, int32_t n_items, int32_t n_blocks,
                          const int32_t* user_bounds, const int32_t* item_bounds,

@@ -345,13 +345,19 @@ static int strata_epoch(const int32_t* user_ids, const int32_t* item_ids,
         set_error("NULL plan or triple array");
         return MF_ERR_INVALID;
     }
-    if ((int64_t)n_blocks * n_blocks >= ((int64_t)1 << 31)) {
+    const int n_cls = strata_classes(flags);       // user-range classes: C*B strata
+    if (n_cls > MF_STRATA_MAX_CLASSES) {
+        set_error("user-range classes %d > %d", n_cls, MF_STRATA_MAX_CLASSES);
+        return MF_ERR_INVALID;
+    }
+    if ((int64_t)n_cls * n_blocks * n_blocks >= ((int64_t)1 << 31)) {
         set_error("n_blocks=%d too large", n_blocks);
         return MF_ERR_INVALID;
     }
     for (int32_t t = 0; t < n_seq; ++t) {
-        if (strata_seq[t] < 0 || strata_seq[t] >= n_blocks) {
-            set_error("strata_seq[%d] = %d out of range [0, %d)", t, strata_seq[t], n_blocks);
+        if (strata_seq[t] < 0 || strata_seq[t] >= n_cls * n_blocks) {
+            set_error("strata_seq[%d] = %d out of range [0, %d)", t, strata_seq[t],
+                      n_cls * n_blocks);
             return MF_ERR_INVALID;
         }
     }

@@ -1,10 +1,13 @@
 // mf_strata.hpp -- the stratified SGD sweep ("strata").
 //
-// Users are cut into B contiguous ranges and items into B contiguous ranges;
-// block (ub, ib) holds the ratings of user range ub x item range ib.  Stratum
-// s is the B blocks (ub = (w + s) mod B, ib = w), w = 0..B-1: they share no
-// user and no item, so one launch applies a whole stratum with workgroup w on
-// block w.  The workgroup stages its item slab Q[ib] (+ b_i) and the user-bias
+// Users are cut into C*B contiguous ranges (C user-range classes, 1 by
+// default) and items into B contiguous ranges; block (ub, ib) holds the
+// ratings of user range ub x item range ib.  Stratum s (s < C*B) is the B
+// blocks (ub = (s + C*w) mod C*B, ib = w), w = 0..B-1: they share no user and
+// no item, so one launch applies a whole stratum with workgroup w on block w.
+// Stratum s only touches the user ranges of class s mod C, so with C > 1 the
+// persistent kernel cycles through the classes and every user-range hand-off
+// has C - 1 whole blocks of slack (see k_sgd_strata_epoch).  The workgroup stages its item slab Q[ib] (+ b_i) and the user-bias
 // slice b_u[ub] in LDS and walks the block's plan (mf_strata_sched.cpp): a
 // D x NS grid, one step per row, one rating SLOT per lane group.  Every user
 // of the block is owned by one slot, so a user row is only ever read and
@@ -70,6 +73,7 @@ struct StrataArgs {
     const int64_t* bstep;    // B*B + 1 step offsets: block (s, w) at s*B + w
     int32_t B;
     int32_t s;
+    int32_t cls;             // user-range classes C (C*B user ranges)
     uint32_t seed;
     int32_t k;
     int32_t upd_user;
@@ -81,7 +85,7 @@ struct StrataArgs {
     T* Dbi;                  //   leaves Q / Bi untouched and writes Dq = Q' - Q, Dbi
     Hyper<T> h;
     int64_t* probe;          // nullable: persistent-kernel phase stamps (mf_strata_set_probe)
-    int32_t* xtab;           // nullable: MF_FLAG_L2_HANDOFF -- per workgroup (base << 4) | XCC id
+    int32_t* xtab;           // nullable: MF_FLAG_L2_HANDOFF -- per workgroup ((base+1) << 4) | XCC id
 };
 
 // first step of block `blk` in this epoch (mirrored by engine.strata_mix)
@@ -538,7 +542,7 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata(StrataArgs<T> A) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int B = A.B;
     const int w = blockIdx.x;
-    const int ub = (w + A.s) % B;
+    const int ub = (A.s + A.cls * w) % (A.cls * B);
     const int64_t blk = (int64_t)A.s * B + w;
     const int ilo = A.ibnd[w], nqi = A.ibnd[w + 1] - ilo;
     const int ulo = A.ubnd[ub], nus = A.ubnd[ub + 1] - ulo;
@@ -563,16 +567,19 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata(StrataArgs<T> A) {
 constexpr int64_t kStrataSpinLimit = (int64_t)1 << 24;
 
 // The stratum order of one persistent launch travels in the kernel arguments
-// (no host-to-device copy per launch): at most one stratum per workgroup, and
-// the persistent kernel runs one workgroup per CU.
-constexpr int kStrataSeqArg = 256;
-struct StrataSeq { int32_t s[kStrataSeqArg]; };
+// (no host-to-device copy per launch): C*B strata of B <= 256 workgroups (one
+// per CU) and C <= MF_STRATA_MAX_CLASSES, 16-bit entries (2 KiB).
+constexpr int kStrataSeqArg = 256 * MF_STRATA_MAX_CLASSES;
+struct StrataSeq { uint16_t s[kStrataSeqArg]; };
 
 // The whole epoch in one launch (MF_FLAG_PERSISTENT): workgroup w keeps item
 // slab w in LDS for every stratum and walks the strata of `seq`; before
-// position t it waits until the workgroup that applied position t - 1 to the
-// same user range, w' = (w + seq[t] - seq[t-1]) mod B, has published
-// done[w'] >= base + t.  The counters only grow (no reset per launch): every
+// position t it waits until the workgroup that applied the same user range
+// last, at position t - C (seq cycles through the C classes; the launcher
+// checks it), w' = (w + j_t - j_{t-C}) mod B with j = seq[.] / C, has
+// published done[w'] >= base + t - C + 1.  With C = 1 that is the previous
+// position, so every block waits for the chain's jitter and the hand-off's
+// latency; with C > 1 the user range was released C - 1 whole blocks ago.  The counters only grow (no reset per launch): every
 // workgroup ends a launch at the same count, so each reads its own counter at
 // the start as `base` (zeroed once with the workspace, and again whenever
 // the caller clears the error word).  Hand-off (cdna_hip_programming.md Guideline 16, R1): the
@@ -598,11 +605,12 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
     const int ilo = A.ibnd[w], nqi = A.ibnd[w + 1] - ilo;
     if (threadIdx.x == 0) {               // this workgroup's count at the end of the last launch
         s_base = __hip_atomic_load(done + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (A.xtab) {                     // publish (launch tag, XCC id)
-            unsigned v;
+        if (A.xtab) {                     // publish (launch tag, XCC id); tag != 0,
+            unsigned v;                   // so a zeroed entry never looks published
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
-            __hip_atomic_store(A.xtab + w, (s_base << 4) | (int)(v & 0xf), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(A.xtab + w, (int)((((unsigned)s_base + 1u) & 0x7FFFFFFu) << 4) |
+                                               (int)(v & 0xf),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     T* Qs = reinterpret_cast<T*>(smem);
@@ -623,24 +631,38 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
     // the 8 residues sit on 8 different XCDs.  With the XCD-class stratum
     // order (checked by the launcher) a user range then moves between
     // workgroups of ONE XCD inside a class and visits every XCD once per
-    // launch, so rows it leaves in an L2 are never read stale there.  Any
-    // doubt (a missing id after the bounded wait, another placement): off.
+    // launch, so rows it leaves in an L2 are never read stale there.  The
+    // verdict must be the same in every workgroup (a plain-storing holder
+    // and a write-through successor on another XCD would race): it depends
+    // only on the complete table, which every workgroup waits for; one that
+    // cannot see it complete within the bounded wait fails the launch (error
+    // word; the caller replays the epoch per stratum) instead of deciding alone.
     bool l2ok = false;
     if (A.xtab) {
         if (threadIdx.x < kWave) {
             const int ln = threadIdx.x;
-            const int want = base << 4;
+            const int want = (int)((((unsigned)base + 1u) & 0x7FFFFFFu) << 4);
             bool ok = true;
+            bool timeout = false;
             for (int64_t spins = 0;; ++spins) {          // wave-uniform
                 bool all = true;
                 for (int j = ln; j < B; j += kWave)
                     all &= (__hip_atomic_load(A.xtab + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &
                             ~0xf) == want;
                 if (__builtin_amdgcn_ballot_w64(!all) == 0) break;
-                if (spins > kStrataSpinLimit) { ok = false; break; }
+                if (spins > kStrataSpinLimit ||
+                    __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                    timeout = true;
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(2);
             }
-            if (ok) {
+            if (timeout) {
+                ok = false;
+                if (ln == 0)
+                    __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (!timeout) {
                 bool bad = false;
                 for (int j = ln; j < B; j += kWave)
                     bad |= (__hip_atomic_load(A.xtab + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xf) !=
@@ -654,23 +676,26 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
                 }
                 ok = __builtin_amdgcn_ballot_w64(bad) == 0;
             }
-            if (ln == 0) s_l2ok = ok ? 1 : 0;
+            if (ln == 0) s_l2ok = timeout ? -1 : ok ? 1 : 0;
         }
         __syncthreads();
+        if (s_l2ok < 0) return;           // the launch failed: nothing applied here
         l2ok = s_l2ok != 0;
     }
+    const int C = A.cls;
     for (int t = 0; t < n_seq; ++t) {
         const int s = seq.s[t];
-        const int ub = (w + s) % B;
+        const int ub = (s + C * w) % (C * B);
         const int ulo = A.ubnd[ub], nus = A.ubnd[ub + 1] - ulo;
         stamp(t, 0);
         if (threadIdx.x == 0) {
             int ab = 0;
-            if (t > 0) {
-                const int wd = (w + s - seq.s[t - 1] + 2 * B) % B;
+            if (t >= C) {
+                // the user range's previous holder: same class, C positions back
+                const int wd = (w + s / C - (int)seq.s[t - C] / C + 2 * B) % B;
                 int64_t spins = 0;
                 while (__hip_atomic_load(done + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                       base + t) {
+                       base + t - C + 1) {
                     __builtin_amdgcn_s_sleep(2);
                     if (++spins > kStrataSpinLimit ||
                         __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
@@ -692,7 +717,7 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
         // the next holder of this user range, w + s_t - s_{t+1}, on this XCD
         // (same residue mod 8, B a multiple of 8): rows stored plainly stay
         // in the L2 it reads; otherwise write-through, as always
-        const bool keep = l2ok && t + 1 < n_seq && ((s - seq.s[t + 1]) & 7) == 0;
+        const bool keep = l2ok && t + 1 < n_seq && ((s - (int)seq.s[t + 1]) & 7) == 0;
         strata_block<T, W, GS, V, KERN, S, true, true, DEPTH, NW>(A, (int64_t)s * B + w, ulo, ilo, Qs,
                                                               Bis, Bus, h, nus, keep);
         __syncthreads();
@@ -738,6 +763,27 @@ inline bool strata_xcd_classes(const int32_t* seq, int32_t n_seq, int32_t B) {
             cur = c;
         }
     }
+    return true;
+}
+
+// user-range classes C from the flags (bits 24..27 = C - 1)
+inline int strata_classes(int32_t flags) {
+    return (int)(((uint32_t)flags >> MF_FLAG_CLASSES_SHIFT) & 0xFu) + 1;
+}
+
+// Does `seq` cycle through the C classes (seq[t] mod C == seq[t mod C] mod C,
+// the first C of distinct classes)?  Then the user range of position t was
+// last used at t - C, which is what the persistent kernel waits for.
+inline bool strata_class_cycle(const int32_t* seq, int32_t n_seq, int C) {
+    if (C == 1) return true;
+    bool seen[MF_STRATA_MAX_CLASSES] = {};
+    for (int32_t t = 0; t < n_seq && t < C; ++t) {
+        const int c = seq[t] % C;
+        if (seen[c]) return false;
+        seen[c] = true;
+    }
+    for (int32_t t = C; t < n_seq; ++t)
+        if (seq[t] % C != seq[t % C] % C) return false;
     return true;
 }
 
@@ -869,6 +915,16 @@ struct StrataRun {
         a.Bu = static_cast<T*>(p.bu); a.Bi = static_cast<T*>(p.bi);
         a.ubnd = p.ubnd; a.ibnd = p.ibnd; a.bstep = p.bstep;
         a.B = p.B; a.seed = p.seed; a.k = p.k; a.upd_user = p.uu; a.upd_item = p.ui;
+        a.cls = strata_classes(p.flags);
+        if (a.cls < 1 || a.cls > MF_STRATA_MAX_CLASSES) {
+            set_error("user-range classes %d outside [1, %d]", a.cls, MF_STRATA_MAX_CLASSES);
+            return MF_ERR_INVALID;
+        }
+        for (int32_t t = 0; t < p.n_seq; ++t)
+            if (p.seq[t] < 0 || p.seq[t] >= a.cls * p.B) {
+                set_error("stratum %d outside [0, %d)", p.seq[t], a.cls * p.B);
+                return MF_ERR_INVALID;
+            }
         a.p_bytes = (uint64_t)p.n_users * (uint64_t)p.k * sizeof(T);
         a.bu_bytes = (uint64_t)p.n_users * sizeof(T);
         // the persistent kernel's 32-bit offsets (strata_block, WT): user ids
@@ -894,7 +950,8 @@ struct StrataRun {
         }
         bool persistent = false;
         if ((p.flags & MF_FLAG_PERSISTENT) && p.ws && p.n_seq <= kStrataSeqArg && u32_ok &&
-            p.ws_bytes >= strata_ws_bytes(p.B, p.n_seq) && a.p_bytes < (uint64_t)kBufDrop) {
+            p.ws_bytes >= strata_ws_bytes(p.B, p.n_seq) && a.p_bytes < (uint64_t)kBufDrop &&
+            strata_class_cycle(p.seq, p.n_seq, a.cls)) {
             // (the deep pipeline exists for the 16- and 8-wave kernels)
             constexpr int kDeep = NW >= 8 ? 2 : 1;
             auto efn = (kDeep == 2 && (p.flags & MF_FLAG_DEEP_PIPE))
@@ -911,12 +968,13 @@ struct StrataRun {
                 // (no line is shared by two users, so no line mixes ranges)
                 const bool lines = ((size_t)p.k * sizeof(T)) % 128 == 0 &&
                                    (reinterpret_cast<uintptr_t>(p.P) & 127) == 0;
-                if ((p.flags & MF_FLAG_L2_HANDOFF) && lines && p.n_seq >= p.B &&
+                if ((p.flags & MF_FLAG_L2_HANDOFF) && lines && p.n_seq >= p.B && a.cls == 1 &&
                     strata_xcd_classes(p.seq, p.n_seq, p.B))
                     a.xtab = err + 1;
                 int32_t nseq = p.n_seq;
                 StrataSeq sq;
-                for (int32_t t = 0; t < kStrataSeqArg; ++t) sq.s[t] = t < nseq ? p.seq[t] : 0;
+                for (int32_t t = 0; t < kStrataSeqArg; ++t)
+                    sq.s[t] = (uint16_t)(t < nseq ? p.seq[t] : 0);
                 if (strata_inject_fail())
                     MF_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(err), 1, 1,
                                                    p.stream));

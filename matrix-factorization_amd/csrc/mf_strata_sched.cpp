@@ -1,9 +1,12 @@
 // mf_strata_sched.cpp -- plan of the slotted stratified sweep
 // (mf_strata_plan_*; kernel: mf_strata.hpp).
 //
-// Ratings are bucketed into B*B blocks (user range x item range); block
-// (ub, ib) belongs to stratum s = (ub - ib) mod B, slot w = ib, and is stored
-// at s*B + w.  Inside a block:
+// Ratings are bucketed into C*B*B blocks: C*B user ranges (C = the number of
+// user-range classes, 1 by default) x B item ranges; block (ub, ib) belongs
+// to stratum s = (ub - C*ib) mod C*B, slot w = ib, and is stored at s*B + w
+// (C = 1: s = (ub - ib) mod B).  Stratum s holds the user ranges of class
+// s mod C only, so strata of different classes share no user (the kernel's
+// slack between hand-offs, mf_strata.hpp).  Inside a block:
 //   1. every user of the block is OWNED by one of NS rating slots (longest
 //      processing time first: users by falling degree onto the least loaded
 //      slot), so all of a user's ratings in the block run on one lane group,
@@ -17,6 +20,8 @@
 // to torch's).
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <functional>
 #include <queue>
@@ -33,8 +38,9 @@ using mf::set_error;
 
 struct mf_strata_plan {
     int32_t B = 0;
+    int32_t C = 1;                  // user-range classes: C*B user ranges
     int32_t NS = 0;
-    std::vector<int64_t> bstep;     // B*B + 1 step offsets
+    std::vector<int64_t> bstep;     // C*B*B + 1 step offsets
     std::vector<int32_t> sched;     // bstep[B*B] * NS positions
 };
 
@@ -149,21 +155,24 @@ bool bounds_ok(const int32_t* b, int32_t nb, int32_t total) {
 
 }  // namespace
 
-extern "C" int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
-                                    int32_t n_users, int32_t n_items, int32_t n_blocks,
-                                    const int32_t* user_bounds, const int32_t* item_bounds,
-                                    int32_t n_slots, mf_strata_plan** plan_out) {
+extern "C" int mf_strata_plan_build_classes(const int32_t* user_ids, const int32_t* item_ids,
+                                            int64_t n, int32_t n_users, int32_t n_items,
+                                            int32_t n_blocks, int32_t n_classes,
+                                            const int32_t* user_bounds,
+                                            const int32_t* item_bounds, int32_t n_slots,
+                                            mf_strata_plan** plan_out) {
     if (!plan_out) {
         set_error("NULL plan_out");
         return MF_ERR_INVALID;
     }
     *plan_out = nullptr;
-    if (n < 0 || n_users < 0 || n_items < 0 || n_blocks < 1 || n_slots < 1 || n_slots > 4096) {
-        set_error("invalid sizes (n=%lld, n_blocks=%d, n_slots=%d)", (long long)n, n_blocks,
-                  n_slots);
+    if (n < 0 || n_users < 0 || n_items < 0 || n_blocks < 1 || n_slots < 1 || n_slots > 4096 ||
+        n_classes < 1 || n_classes > MF_STRATA_MAX_CLASSES) {
+        set_error("invalid sizes (n=%lld, n_blocks=%d, n_classes=%d, n_slots=%d)", (long long)n,
+                  n_blocks, n_classes, n_slots);
         return MF_ERR_INVALID;
     }
-    if ((int64_t)n_blocks * n_blocks >= ((int64_t)1 << 31) || n > INT32_MAX) {
+    if ((int64_t)n_classes * n_blocks * n_blocks >= ((int64_t)1 << 31) || n > INT32_MAX) {
         set_error("n_blocks=%d / n=%lld too large", n_blocks, (long long)n);
         return MF_ERR_INVALID;
     }
@@ -171,17 +180,28 @@ extern "C" int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item
         set_error("NULL argument");
         return MF_ERR_INVALID;
     }
-    const int32_t B = n_blocks;
-    if (!bounds_ok(user_bounds, B, n_users) || !bounds_ok(item_bounds, B, n_items)) {
-        set_error("user/item bounds must rise from 0 to n_users/n_items over n_blocks+1 entries");
+    const int32_t B = n_blocks, C = n_classes, CB = n_classes * n_blocks;
+    if (!bounds_ok(user_bounds, CB, n_users) || !bounds_ok(item_bounds, B, n_items)) {
+        set_error("user/item bounds must rise from 0 to n_users/n_items over "
+                  "n_classes*n_blocks+1 / n_blocks+1 entries");
         return MF_ERR_INVALID;
     }
+    const bool tm = std::getenv("MF_PLAN_TIMING") != nullptr;     // diagnostics
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto t0 = now();
+    auto lap = [&](const char* what) {
+        if (!tm) return;
+        const auto t1 = now();
+        std::fprintf(stderr, "[mf_strata_plan] %s %.3f s\n", what,
+                     std::chrono::duration<double>(t1 - t0).count());
+        t0 = t1;
+    };
     std::vector<int32_t> ub_of(n_users), ib_of(n_items);
-    for (int32_t b = 0; b < B; ++b) {
+    for (int32_t b = 0; b < CB; ++b)
         for (int32_t x = user_bounds[b]; x < user_bounds[b + 1]; ++x) ub_of[x] = b;
+    for (int32_t b = 0; b < B; ++b)
         for (int32_t x = item_bounds[b]; x < item_bounds[b + 1]; ++x) ib_of[x] = b;
-    }
-    const int64_t BB = (int64_t)B * B;
+    const int64_t BB = (int64_t)CB * B;
     const int T = mf::host_threads();
     {   // first rating (lowest index) with an id out of range, if any
         std::atomic<int64_t> first_bad{n};
@@ -204,16 +224,18 @@ extern "C" int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item
         }
     }
     // ratings by block (stable): block of (user range ub, item range w) is
-    // stored at s*B + w with s = (ub - w) mod B
+    // stored at s*B + w with s = (ub - C*w) mod C*B
     std::vector<int32_t> bucket(n);
     std::vector<int64_t> boff;
     mf::partition_rows(
         n, (int)BB, T,
         [&](int64_t j) {
             const int32_t w = ib_of[item_ids[j]];
-            return (int)((int64_t)((ub_of[user_ids[j]] - w + B) % B) * B + w);
+            const int64_t sv = (((int64_t)ub_of[user_ids[j]] - (int64_t)C * w) % CB + CB) % CB;
+            return (int)(sv * B + w);
         },
         boff, [&](int64_t d, int64_t j) { bucket[d] = (int32_t)j; });
+    lap("validate + partition");
 
     // plan the blocks in chunks of 64 on worker threads
     const int64_t CH = 64;
@@ -228,7 +250,7 @@ extern "C" int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item
             if (c >= nch) break;
             for (int64_t b = c * CH; b < std::min(BB, (c + 1) * CH); ++b) {
                 const int32_t s = (int32_t)(b / B), w = (int32_t)(b % B);
-                const int32_t ub = (w + s) % B;
+                const int32_t ub = (int32_t)(((int64_t)s + (int64_t)C * w) % CB);
                 steps[b] = plan_block(user_ids, item_ids, bucket.data() + boff[b],
                                       (int32_t)(boff[b + 1] - boff[b]), item_bounds[w],
                                       item_bounds[w + 1] - item_bounds[w], user_bounds[ub],
@@ -242,6 +264,7 @@ extern "C" int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item
     for (unsigned t = 1; t < nt; ++t) th.emplace_back(worker);
     worker();
     for (auto& t : th) t.join();
+    lap("plan blocks");
 
     auto* plan = new (std::nothrow) mf_strata_plan;
     if (!plan) {
@@ -249,6 +272,7 @@ extern "C" int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item
         return MF_ERR_NOMEM;
     }
     plan->B = B;
+    plan->C = C;
     plan->NS = n_slots;
     plan->bstep.resize(BB + 1);
     plan->bstep[0] = 0;
@@ -258,8 +282,17 @@ extern "C" int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item
         plan->sched.insert(plan->sched.end(), g.begin(), g.end());
         std::vector<int32_t>().swap(g);
     }
+    lap("assemble");
     *plan_out = plan;
     return MF_OK;
+}
+
+extern "C" int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
+                                    int32_t n_users, int32_t n_items, int32_t n_blocks,
+                                    const int32_t* user_bounds, const int32_t* item_bounds,
+                                    int32_t n_slots, mf_strata_plan** plan_out) {
+    return mf_strata_plan_build_classes(user_ids, item_ids, n, n_users, n_items, n_blocks, 1,
+                                        user_bounds, item_bounds, n_slots, plan_out);
 }
 
 extern "C" int64_t mf_strata_plan_positions(const mf_strata_plan* plan) {

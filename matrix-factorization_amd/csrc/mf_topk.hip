@@ -751,7 +751,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm(MmArgs A) {
     // past k meet zero A operands
     auto load_b = [&](int it0, float (&b)[SEG], float& bi) __attribute__((always_inline)) {
         const int n = it0 + c;
-        const int nn = n < iend ? n : ibeg;
+        const int nn = n < iend ? n : (ibeg < iend ? ibeg : 0);   // empty split: row 0
         const float* qr = A.Q + (int64_t)nn * k;
         bi = A.Bi[nn];                   // first: waiting for it waits for nothing else
 #pragma unroll
@@ -1053,7 +1053,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
     __syncthreads();                                     // the setup's LDS words
     auto load_b = [&](int it0, float (&b)[SEG], float& bi) __attribute__((always_inline)) {
         const int n = it0 + c;
-        const int nn = n < iend ? n : ibeg;
+        const int nn = n < iend ? n : (ibeg < iend ? ibeg : 0);   // empty split: row 0
         const float* qr = A.Q + (int64_t)nn * k;
         bi = A.Bi[nn];
 #pragma unroll
@@ -1220,7 +1220,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
         load_b(ibeg + 32, b, bi);
         auto load_half = [&](int it0, int part) __attribute__((always_inline)) {
             const int n = it0 + c;
-            const int nn = n < iend ? n : ibeg;
+            const int nn = n < iend ? n : (ibeg < iend ? ibeg : 0);   // empty split: row 0
             const float* qr = A.Q + (int64_t)nn * k;
             if (part == 0) bi = A.Bi[nn];
             // the first part: whole float4 groups among the columns the

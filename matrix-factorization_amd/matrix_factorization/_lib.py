@@ -25,6 +25,8 @@ MF_FLAG_DEEP_PIPE = 32
 MF_FLAG_NO_COOP = 64
 MF_FLAG_NARROW = 128
 MF_FLAG_L2_HANDOFF = 256
+MF_FLAG_CLASSES_SHIFT = 24       # bits 24..27: user-range classes - 1
+MF_STRATA_MAX_CLASSES = 4
 MF_ERR_CAPACITY = 3
 MF_DELTA_TAKE, MF_DELTA_APPLY = 0, 1
 KERNEL_CODES = {"linear": MF_LINEAR, "sigmoid": MF_SIGMOID, "rbf": MF_RBF}
@@ -110,6 +112,8 @@ SIGNATURES = {
     "mf_sched_slices": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P, _P]),
     "mf_strata_plan_build": (ctypes.c_int, [
         _P, _P, _I64, _I32, _I32, _I32, _P, _P, _I32, _P]),
+    "mf_strata_plan_build_classes": (ctypes.c_int, [
+        _P, _P, _I64, _I32, _I32, _I32, _I32, _P, _P, _I32, _P]),
     "mf_strata_plan_positions": (_I64, [_P]),
     "mf_strata_plan_fetch": (ctypes.c_int, [_P, _P, _P]),
     "mf_strata_plan_free": (None, [_P]),

@@ -68,7 +68,7 @@ class ALSMF(KernelMF):
                                               (self.n_users, self.n_factors))
         self.item_features = np.random.normal(self.init_mean, self.init_sd,
                                               (self.n_items, self.n_factors))
-        eng = self._make_engine(X)
+        eng = self._make_engine(X, len(self.user_features), len(self.item_features))
         eng.load_params(self.user_features, self.item_features,
                         self.user_biases, self.item_biases)
         self.train_rmse = self._run(eng, self.n_epochs, False, self.verbose)
@@ -91,7 +91,7 @@ class ALSMF(KernelMF):
         new_user_features = np.random.normal(self.init_mean, self.init_sd,
                                              (len(new_users), self.n_factors))
         self.user_features = np.concatenate((self.user_features, new_user_features), axis=0)
-        eng = self._make_engine(X)
+        eng = self._make_engine(X, len(self.user_features), len(self.item_features))
         eng.load_params(self.user_features, self.item_features,
                         self.user_biases, self.item_biases)
         self.train_rmse = self._run(eng, n_epochs, True, verbose)

@@ -221,9 +221,10 @@ def rotation_range(rank: int, off: int, s: int, world: int) -> int:
     return (rank + off + s) % world
 
 
-def rotation_draws(draw: int, rank: int, c: int, nb: int):
+def rotation_draws(draw: int, rank: int, c: int, nb):
     """Stratum order and step rotation of rank ``rank``'s sub-block with item
-    range ``c`` in the epoch with ``draw`` (reproducible per sub-block)."""
+    range ``c`` in the epoch with ``draw`` (reproducible per sub-block);
+    ``nb`` = the strata plan (or its B)."""
     rs = np.random.RandomState([int(draw) & 0x7FFFFFFF, rank, c])
     return stratum_order(rs, nb), int(rs.randint(0, 2**31 - 1))
 
@@ -400,7 +401,7 @@ def rotation_epoch(engine: SGDEngine, rot: RotationExchange, draw: int, lr: floa
     receives each sub-epoch's kernel launch count (1 = persistent;
     synchronises after every sub-epoch)."""
     world, rank = rot.world, rot.rank
-    nb = engine.strata.B
+    nb = engine.strata
     off = rotation_offset(epoch, world)
 
     def mark(kind, fn):
@@ -426,7 +427,7 @@ def rotation_epoch(engine: SGDEngine, rot: RotationExchange, draw: int, lr: floa
     c_final = [rotation_range(r, off, world - 1, world) for r in range(world)]
     if rot.overlap and sse_slot is not None:
         mark("gather", lambda: rot.snapshot_sse(c_final, sse_slot,
-                                                sse_blocks_beside(engine, nb), sse_timing))
+                                                sse_blocks_beside(engine, nb.B), sse_timing))
     else:
         mark("gather", lambda: rot.gather(c_final))
 
@@ -452,7 +453,8 @@ class RotationReplay:
     def __init__(self, u, i, r, n_users: int, n_items: int, world: int, n_factors: int,
                  kernel: str, dtype: str, device, gamma: float = 0.0, min_rating: float = 0.0,
                  max_rating: float = 5.0, global_mean: float = 0.0,
-                 n_blocks: Optional[int] = None, waves: Optional[int] = None, engine_cls=None):
+                 n_blocks: Optional[int] = None, waves: Optional[int] = None, engine_cls=None,
+                 classes: Optional[int] = None):
         make = SGDEngine if engine_cls is None else engine_cls
         self.world = world
         self.bounds = shard_users(u, n_users, world)
@@ -467,9 +469,10 @@ class RotationReplay:
                      gamma=gamma, min_rating=min_rating, max_rating=max_rating,
                      global_mean=global_mean)
             if waves is None:
-                e.prepare_strata(n_blocks=n_blocks, item_bounds=self.ilo)
+                e.prepare_strata(n_blocks=n_blocks, item_bounds=self.ilo, classes=classes)
             else:
-                e.prepare_strata(n_blocks=n_blocks, waves=waves, item_bounds=self.ilo)
+                e.prepare_strata(n_blocks=n_blocks, waves=waves, item_bounds=self.ilo,
+                                 classes=classes)
             self.engines.append(e)
         # one B for every rank (each rank's plans draw their strata from it)
         self.B = [e.strata.B for e in self.engines]
@@ -492,7 +495,7 @@ class RotationReplay:
         for s in range(W):
             for rank, e in enumerate(self.engines):
                 c = rotation_range(rank, off, s, W)
-                seq, seed = rotation_draws(draw, rank, c, e.strata.B)
+                seq, seed = rotation_draws(draw, rank, c, e.strata)
                 t = e.epoch_phase(c, seq, seed, lr, reg, update_user, update_item,
                                   timing=timing, persistent=persistent)
                 if timing:
@@ -507,7 +510,7 @@ class RotationReplay:
         for s in range(W):
             for rank, e in enumerate(self.engines):
                 c = rotation_range(rank, off, s, W)
-                seq, seed = rotation_draws(draw, rank, c, e.strata.B)
+                seq, seed = rotation_draws(draw, rank, c, e.strata)
                 parts.append(self.gidx[rank][e.strata.phase_order(c, seq, seed)])
         return np.concatenate(parts).astype(np.int64)
 
@@ -527,8 +530,9 @@ class RotationReplay:
                 e0.bi.cpu().numpy().astype(np.float64))
 
 
-def epoch_draws(rs: np.random.RandomState, nb: int, strata: bool):
-    """Stratum (colour) order and step rotation of one epoch."""
+def epoch_draws(rs: np.random.RandomState, nb, strata: bool):
+    """Stratum (colour) order and step rotation of one epoch (``nb``: the
+    strata plan, or the colour count)."""
     seq = stratum_order(rs, nb) if strata else rs.permutation(nb).astype(np.int32)
     rot = int(rs.randint(0, 2**31 - 1)) if strata else 0
     return seq, rot
@@ -550,7 +554,7 @@ def sharded_epochs(engine: SGDEngine, exchange: Optional[ReplicaExchange], n_epo
     if strata:
         if engine.strata is None:
             engine.prepare_strata(n_blocks=n_blocks)
-        nb = engine.strata.B
+        nb = engine.strata
     else:
         if engine.colored is None:
             engine.prepare_colored()
@@ -667,13 +671,13 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
         eng.prepare_strata(item_bounds=ilo)
         # the RMSE pass of epoch e beside epoch e+1's sub-epochs (side stream)
         rot = RotationExchange(eng, ilo, group, overlap=True)
-        nb = eng.strata.B
+        nb = eng.strata
     else:
         ex = ReplicaExchange(eng, group)
         ex.bind(Q0, bi0)
         if strata:
             eng.prepare_strata()
-            nb = eng.strata.B
+            nb = eng.strata
         else:
             eng.prepare_colored()
             nb = len(eng.colored) - 1

@@ -26,6 +26,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import sys
 import warnings
 from typing import Optional, Sequence, Tuple
 
@@ -144,12 +145,15 @@ def strata_mix(seed: int, blk: int) -> int:
     return x
 
 
-def balanced_bounds(ids: np.ndarray, m: int, n_blocks: int, by_count: bool = True) -> np.ndarray:
+def balanced_bounds(ids: np.ndarray, m: int, n_blocks: int, by_count: bool = True,
+                    cum: Optional[np.ndarray] = None) -> np.ndarray:
     """``n_blocks`` contiguous id ranges over [0, m): equal rating counts
-    (``by_count``) or equal id counts."""
+    (``by_count``) or equal id counts.  ``cum``: the cumulative rating count
+    per id, if already known (SGDEngine.degree_cum)."""
     if not by_count or len(ids) == 0:
         return (np.arange(n_blocks + 1, dtype=np.int64) * m // n_blocks).astype(np.int32)
-    cum = np.cumsum(np.bincount(ids, minlength=m).astype(np.int64))
+    if cum is None:
+        cum = np.cumsum(np.bincount(ids, minlength=m).astype(np.int64))
     targets = np.arange(1, n_blocks, dtype=np.int64) * cum[-1] // n_blocks
     cuts = np.searchsorted(cum, targets, side="left") + 1
     b = np.concatenate([[0], np.minimum(cuts, m), [m]]).astype(np.int64)
@@ -157,14 +161,16 @@ def balanced_bounds(ids: np.ndarray, m: int, n_blocks: int, by_count: bool = Tru
 
 
 class StrataPlan:
-    """Host + device form of a mf_strata_plan: B x B blocks, each a grid of
-    ``n_steps`` x ``NS`` rating slots (``sched``: rating index per position,
-    -1 = idle slot)."""
+    """Host + device form of a mf_strata_plan: C*B user ranges x B item
+    ranges (C = ``classes`` user-range classes, 1 = the plain B x B plan),
+    C*B strata of B blocks, each block a grid of ``n_steps`` x ``NS`` rating
+    slots (``sched``: rating index per position, -1 = idle slot)."""
 
     narrow = False      # built for the narrow 4-wave kernels (MF_FLAG_NARROW)
 
-    def __init__(self, B, NS, ubnd, ibnd, bstep, sched):
+    def __init__(self, B, NS, ubnd, ibnd, bstep, sched, classes=1):
         self.B, self.NS = int(B), int(NS)
+        self.classes = int(classes)
         self.ubnd, self.ibnd, self.bstep, self.sched = ubnd, ibnd, bstep, sched
         self.max_items = int(np.diff(ibnd).max()) if B else 0
         self.max_users = int(np.diff(ubnd).max()) if B else 0
@@ -189,6 +195,11 @@ class StrataPlan:
     @property
     def n_positions(self) -> int:
         return len(self.sched)
+
+    @property
+    def n_strata(self) -> int:
+        """Strata of one epoch (launches of the per-stratum form)."""
+        return self.classes * self.B
 
     @property
     def n_ratings(self) -> int:
@@ -242,6 +253,7 @@ class PhasedStrata:
         self.phases, self.idx = phases, idx
         self.ilo = np.asarray(ilo, np.int64)
         self.B, self.NS = phases[0].B, phases[0].NS
+        self.classes = phases[0].classes
         self.narrow = phases[0].narrow
         self.max_items = max(pl.max_items for pl in phases)
         self.max_users = max(pl.max_users for pl in phases)
@@ -249,6 +261,10 @@ class PhasedStrata:
     @property
     def n_positions(self) -> int:
         return sum(pl.n_positions for pl in self.phases)
+
+    @property
+    def n_strata(self) -> int:
+        return self.classes * self.B
 
     @property
     def n_steps(self) -> np.ndarray:
@@ -271,8 +287,9 @@ class PhasedStrata:
 
 
 def sched_strata(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int, n_blocks: int,
-                 ubnd: np.ndarray, ibnd: np.ndarray, n_slots: int):
-    """mf_strata_plan_build + fetch: (sched, block step offsets)."""
+                 ubnd: np.ndarray, ibnd: np.ndarray, n_slots: int, classes: int = 1):
+    """mf_strata_plan_build_classes + fetch: (sched, block step offsets);
+    ``ubnd`` has classes * n_blocks + 1 entries."""
     n = len(u)
     u = np.ascontiguousarray(u, np.int32)
     i = np.ascontiguousarray(i, np.int32)
@@ -280,12 +297,12 @@ def sched_strata(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int, n_blo
     ibnd = np.ascontiguousarray(ibnd, np.int32)
     lib = _lib.load()
     handle = ctypes.c_void_p()
-    _lib.call("mf_strata_plan_build", _np(u), _np(i), n, n_users, n_items, n_blocks,
-              _np(ubnd), _np(ibnd), n_slots, ctypes.byref(handle))
+    _lib.call("mf_strata_plan_build_classes", _np(u), _np(i), n, n_users, n_items, n_blocks,
+              int(classes), _np(ubnd), _np(ibnd), n_slots, ctypes.byref(handle))
     try:
         npos = int(lib.mf_strata_plan_positions(handle))
         sched = np.empty(max(npos, 1), np.int32)
-        bstep = np.empty(n_blocks * n_blocks + 1, np.int64)
+        bstep = np.empty(int(classes) * n_blocks * n_blocks + 1, np.int64)
         _lib.call("mf_strata_plan_fetch", handle, _np(sched), _np(bstep))
     finally:
         lib.mf_strata_plan_free(handle)
@@ -313,9 +330,10 @@ ROTATE_PER_B2 = 1024.0
 
 
 def choose_strata_blocks(u, i, n_users, n_items, k, dcode, max_blocks=None,
-                         per_b2: float = STRATA_PER_B2):
+                         per_b2: float = STRATA_PER_B2, classes: int = 1, cums=(None, None)):
     """B and the user / item bounds: B ~ sqrt(n / per_b2) capped at 256 (one
-    workgroup per CU), raised until the largest block's LDS image fits."""
+    workgroup per CU), raised until the largest block's LDS image fits;
+    ``classes`` * B user ranges (user-range classes)."""
     lib = _lib.load()
     n = len(u)
     B = int(min(256, max(1, np.sqrt(n / float(per_b2)))))
@@ -323,9 +341,9 @@ def choose_strata_blocks(u, i, n_users, n_items, k, dcode, max_blocks=None,
         B = min(B, int(max_blocks))
     limit = lib.mf_strata_lds_limit()
     while True:
-        ub = balanced_bounds(u, n_users, B)
+        ub = balanced_bounds(u, n_users, classes * B, cum=cums[0])
         for by_count in (True, False):
-            ib = balanced_bounds(i, n_items, B, by_count)
+            ib = balanced_bounds(i, n_items, B, by_count, cum=cums[1])
             need = lib.mf_strata_lds_bytes(int(np.diff(ib).max()), int(np.diff(ub).max()),
                                            k, dcode)
             if need <= limit:
@@ -341,7 +359,9 @@ XCD_CLASSES = 8                  # gfx950: workgroups dealt round-robin over 8 X
 class _HipBlock:
     """A physically contiguous device allocation, exposed to torch through
     __cuda_array_interface__ (torch keeps this object alive as long as the
-    tensor's storage, and the block is freed with it)."""
+    tensor's storage, and the block is freed with it).  The block is not
+    torch's: it does not show in torch.cuda.memory_allocated() or the caching
+    allocator's statistics."""
 
     _hip = None
 
@@ -363,9 +383,15 @@ class _HipBlock:
                                          "strides": None}
 
     def __del__(self):
-        if getattr(self, "ptr", None) is not None and _HipBlock._hip is not None:
+        # at interpreter shutdown the HIP runtime (or ctypes) may already be
+        # gone: the process exit releases the memory then
+        if getattr(self, "ptr", None) is None or _HipBlock._hip is None or sys.is_finalizing():
+            return
+        try:
             _HipBlock._hip.hipFree(self.ptr)
-            self.ptr = None
+        except Exception:            # noqa: BLE001 -- never raise from a finaliser
+            pass
+        self.ptr = None
 
 
 def _contiguous_empty(shape, dtype, dev) -> Optional[torch.Tensor]:
@@ -383,11 +409,17 @@ def _contiguous_empty(shape, dtype, dev) -> Optional[torch.Tensor]:
     return t
 
 
-def stratum_order(rs, nb: int, mode: Optional[str] = None) -> np.ndarray:
+def stratum_order(rs, nb, mode: Optional[str] = None, classes: Optional[int] = None) -> np.ndarray:
     """The stratum order of one epoch, drawn from ``rs`` (a RandomState or
-    the ``np.random`` module).
+    the ``np.random`` module).  ``nb``: B, or a strata plan (its B and its
+    user-range classes C).
 
-    random: a uniform permutation of the B strata.
+    random: a uniform permutation of the B strata.  With C > 1 user-range
+            classes (C*B strata, stratum s of class s mod C): the classes in
+            a random order, each class's B strata in a random order, dealt
+            round-robin -- position t holds a stratum of class
+            cls[t mod C], so a user range is used again only C positions
+            later (the persistent kernel's slack).
     xcd:    the strata grouped by s mod 8, the classes in random order and each
             class's strata in random order (B a multiple of 8; else random).
             Stratum t's user range r comes from the workgroup w' = w + s_t -
@@ -396,6 +428,17 @@ def stratum_order(rs, nb: int, mode: Optional[str] = None) -> np.ndarray:
             over the XCDs) and the rows come from its L2 -- every order is a
             sequential order, the choice changes which one.
     """
+    if hasattr(nb, "B"):
+        classes = nb.classes if classes is None else classes
+        nb = nb.B
+    classes = int(classes or 1)
+    if classes > 1:
+        cls = rs.permutation(classes)
+        per = [rs.permutation(nb) for _ in range(classes)]
+        t = np.arange(classes * nb)
+        c = cls[t % classes]
+        j = np.stack(per)[c, t // classes]
+        return (c + classes * j).astype(np.int32)
     mode = mode or os.environ.get("MF_STRATA_ORDER", "random")
     if mode == "xcd" and nb % XCD_CLASSES == 0 and nb > XCD_CLASSES:
         cls = rs.permutation(XCD_CLASSES)
@@ -566,10 +609,28 @@ class SGDEngine:
         self.colored = offs
         return len(offs) - 1
 
+    # user-range classes of the strata plans (StrataPlan.classes): None = 1;
+    # env MF_STRATA_CLASSES overrides
+    strata_classes: Optional[int] = None
+
+    def _classes(self, classes: Optional[int]) -> int:
+        if classes is None and os.environ.get("MF_STRATA_CLASSES"):
+            classes = int(os.environ["MF_STRATA_CLASSES"])
+        if classes is None:
+            classes = self.strata_classes
+        if classes is None:
+            classes = 1
+        classes = int(classes)
+        if not 1 <= classes <= _lib.MF_STRATA_MAX_CLASSES:
+            raise ValueError(f"strata classes must be in [1, {_lib.MF_STRATA_MAX_CLASSES}], "
+                             f"got {classes}")
+        return classes
+
     def prepare_strata(self, n_blocks: Optional[int] = None,
                        waves: Optional[int] = None,
                        phases: Optional[int] = None,
-                       item_bounds: Optional[np.ndarray] = None) -> "StrataPlan":
+                       item_bounds: Optional[np.ndarray] = None,
+                       classes: Optional[int] = None) -> "StrataPlan":
         """Build the stratified plan once and store a padded copy of the
         ratings in plan order (block-major, step-major, slot-minor).  The
         host arrays keep the original rating order.
@@ -588,9 +649,15 @@ class SGDEngine:
 
         ``item_bounds``: the phases' item ranges given explicitly (len P + 1
         ascending ids from 0 to n_items) -- the item ranges of the rotation
-        schedule (distributed.item_ranges); a PhasedStrata even for P = 1."""
+        schedule (distributed.item_ranges); a PhasedStrata even for P = 1.
+
+        ``classes``: user-range classes C (C*B user ranges, C*B strata per
+        epoch; the persistent kernel then hands a user range over with C - 1
+        blocks of slack).  None = ``strata_classes`` / env
+        MF_STRATA_CLASSES, else 1."""
         if self.colored is not None or self.strata is not None:
             raise RuntimeError("ratings already permuted by another schedule")
+        classes = self._classes(classes)
         env = os.environ.get("MF_STRATA_WAVES")
         if waves is None and env in ("4", "8", "16"):
             waves = int(env)
@@ -600,34 +667,46 @@ class SGDEngine:
                     or np.any(np.diff(ilo) < 0)):
                 raise ValueError("item_bounds must ascend from 0 to n_items")
             self.strata = self._prepare_phased(len(ilo) - 1, n_blocks, waves, ilo,
-                                               per_b2=ROTATE_PER_B2)
+                                               per_b2=ROTATE_PER_B2, classes=classes)
             return self.strata
         if phases is None and os.environ.get("MF_STRATA_PHASES"):
             phases = int(os.environ["MF_STRATA_PHASES"])
         bounds = None
         if phases is None and n_blocks is None:
-            phases, n_blocks, bounds = self._item_phases()
+            phases, n_blocks, bounds = self._item_phases(classes)
         if phases is not None and int(phases) > 1:
-            plan = self._prepare_phased(int(phases), n_blocks, waves)
+            plan = self._prepare_phased(int(phases), n_blocks, waves, classes=classes)
         else:
             plan = self._build_plan(self.u_host, self.i_host, self.n_items, n_blocks, waves,
-                                    bounds)
+                                    bounds, classes)
             plan.to_device(self.u, self.i, self.r, self.dev)
         self.strata = plan
         return plan
+
+    def degree_cum(self, side: str) -> Optional[np.ndarray]:
+        """Cumulative rating count per user (or item) id, from a histogram of
+        the uploaded ids on the device (np.bincount of 10^8 host ids takes
+        a large part of a second; the plan's balanced bounds need it)."""
+        ids = self.u if side == "user" else self.i
+        m = self.n_users if side == "user" else self.n_items
+        if self.n == 0 or ids is None:
+            return None
+        h = torch.bincount(ids, minlength=m)
+        return torch.cumsum(h, 0).cpu().numpy().astype(np.int64)
 
     def _cus(self) -> int:
         if self.dev.type != "cuda":
             return 256
         return int(torch.cuda.get_device_properties(self.dev).multi_processor_count)
 
-    def _item_phases(self):
+    def _item_phases(self, classes: int = 1):
         """(P, B, bounds): 1 phase and the default B with its user / item
         bounds when the plan's workgroups fit one per CU; else the fewest item
         phases whose common B does (see PhasedStrata), bounds None."""
         cus = self._cus()
         B, ub, ib = choose_strata_blocks(self.u_host, self.i_host, self.n_users, self.n_items,
-                                         self.k, self.dcode)
+                                         self.k, self.dcode, classes=classes,
+                                         cums=(self.degree_cum("user"), self.degree_cum("item")))
         if B <= cus or self.n == 0:
             return 1, B, (ub, ib)
         for P in range(2, 9):
@@ -637,20 +716,23 @@ class SGDEngine:
                 m = (self.i_host >= ilo[p]) & (self.i_host < ilo[p + 1])
                 b, _, _ = choose_strata_blocks(self.u_host[m], self.i_host[m] - ilo[p],
                                                self.n_users, int(ilo[p + 1] - ilo[p]),
-                                               self.k, self.dcode, max_blocks=cus)
+                                               self.k, self.dcode, max_blocks=cus,
+                                               classes=classes)
                 Bp = max(Bp, b)
             if Bp <= cus:
                 return P, Bp, None
         return 1, B, (ub, ib)               # no persistent form: one launch per stratum
 
-    def _build_plan(self, u, i, n_items, n_blocks, waves, bounds=None) -> "StrataPlan":
+    def _build_plan(self, u, i, n_items, n_blocks, waves, bounds=None,
+                    classes: int = 1) -> "StrataPlan":
         if bounds is not None:
             B, (ub, ib) = int(n_blocks), bounds
         elif n_blocks is None:
-            B, ub, ib = choose_strata_blocks(u, i, self.n_users, n_items, self.k, self.dcode)
+            B, ub, ib = choose_strata_blocks(u, i, self.n_users, n_items, self.k, self.dcode,
+                                             classes=classes)
         else:
             B = int(n_blocks)
-            ub = balanced_bounds(u, self.n_users, B)
+            ub = balanced_bounds(u, self.n_users, classes * B)
             ib = balanced_bounds(i, n_items, B)
             need = _lib.load().mf_strata_lds_bytes(int(np.diff(ib).max()), int(np.diff(ub).max()),
                                                    self.k, self.dcode)
@@ -666,19 +748,19 @@ class SGDEngine:
                     raise ValueError(f"no {wv}-wave strata kernel for n_factors={self.k}, "
                                      f"dtype={self.dtype}")
                 continue
-            sched, bstep = sched_strata(u, i, self.n_users, n_items, B, ub, ib, ns)
+            sched, bstep = sched_strata(u, i, self.n_users, n_items, B, ub, ib, ns, classes)
             cost = int(bstep[-1]) * wv
             if best is None or cost < best[0]:
                 best = (cost, ns, sched, bstep)
             if waves is None and wv == 16 and n / max(len(sched), 1) >= 0.7:
                 break                       # well filled: the 16-wave plan it is
         _, ns, sched, bstep = best
-        plan = StrataPlan(B, ns, ub, ib, bstep, sched)
+        plan = StrataPlan(B, ns, ub, ib, bstep, sched, classes)
         plan.narrow = waves == 4
         return plan
 
     def _prepare_phased(self, P: int, n_blocks, waves, ilo=None,
-                        per_b2: float = STRATA_PER_B2) -> PhasedStrata:
+                        per_b2: float = STRATA_PER_B2, classes: int = 1) -> PhasedStrata:
         if ilo is None:
             ilo = balanced_bounds(self.i_host, self.n_items, P).astype(np.int64)
         # one pass over the ratings: each phase's indices in rating order
@@ -689,12 +771,14 @@ class SGDEngine:
         if n_blocks is None:                # one B for every phase: the largest needed
             n_blocks = max(choose_strata_blocks(self.u_host[ix], self.i_host[ix] - ilo[p],
                                                 self.n_users, max(int(ilo[p + 1] - ilo[p]), 1),
-                                                self.k, self.dcode, per_b2=per_b2)[0]
+                                                self.k, self.dcode, per_b2=per_b2,
+                                                classes=classes)[0]
                            for p, ix in enumerate(idx))
         plans = []
         for p, ix in enumerate(idx):
             ui, ii = self.u_host[ix], self.i_host[ix] - int(ilo[p])
-            pl = self._build_plan(ui, ii, int(ilo[p + 1] - ilo[p]), n_blocks, waves)
+            pl = self._build_plan(ui, ii, int(ilo[p + 1] - ilo[p]), n_blocks, waves,
+                                  classes=classes)
             if waves is None:               # phase 0 picks the kernel shape for all
                 waves = 16 if pl.NS == strata_slots(self.k, self.dcode, 16) else 8
             t = torch.from_numpy(ix).to(self.dev)
@@ -730,14 +814,15 @@ class SGDEngine:
     def epoch_strata(self, seq: Optional[np.ndarray], seed: int, lr: float, reg: float,
                      update_user: bool = True, update_item: bool = True, timing=False,
                      persistent: Optional[bool] = None, delta=None):
-        """Apply the strata listed in ``seq`` (a permutation of range(B) is
-        one epoch) with step rotation ``seed``.  ``delta`` = (dQ, db_i)
+        """Apply the strata listed in ``seq`` (a permutation of
+        range(n_strata) is one epoch; stratum_order draws one) with step
+        rotation ``seed``.  ``delta`` = (dQ, db_i)
         device tensors: delta-out form (mf_sgd_epoch_strata_delta) -- Q and
         b_i keep their values, the epoch's item update goes to the deltas."""
         pl = self.strata
         if pl is None:
             raise RuntimeError("call prepare_strata() first")
-        seq = (np.arange(pl.B, dtype=np.int32) if seq is None
+        seq = (np.arange(pl.n_strata, dtype=np.int32) if seq is None
                else np.ascontiguousarray(seq, np.int32))
         if isinstance(pl, PhasedStrata):
             return self._epoch_phased(pl, seq, seed, lr, reg, update_user, update_item, timing,
@@ -758,6 +843,7 @@ class SGDEngine:
             flags |= _lib.MF_FLAG_NO_COOP
         if pl.narrow:
             flags |= _lib.MF_FLAG_NARROW
+        flags |= (pl.classes - 1) << _lib.MF_FLAG_CLASSES_SHIFT
         # user rows handed over inside an XCD through its L2 (needs the
         # XCD-class stratum order; the launcher checks the order, the kernel
         # the placement) -- DESIGN.md section 5
@@ -793,7 +879,7 @@ class SGDEngine:
         pl = self.strata
         if not isinstance(pl, PhasedStrata):
             raise RuntimeError("epoch_phase needs prepare_strata(item_bounds=...) or phases")
-        seq = (np.arange(pl.B, dtype=np.int32) if seq is None
+        seq = (np.arange(pl.n_strata, dtype=np.int32) if seq is None
                else np.ascontiguousarray(seq, np.int32))
         sub = pl.phases[p]
         lo, hi = int(pl.ilo[p]), int(pl.ilo[p + 1])
@@ -1257,6 +1343,32 @@ class FactorALS:
         self.sweep_items(reg)
 
 
+class _ErrorPoll:
+    """Non-blocking look at the persistent sweep's sticky error word: after
+    each epoch's launch a copy of the word goes to pinned host memory behind
+    an event; ``failed()`` reads the copy only once that event has completed
+    (never waits), so a failure in epoch e is seen a few epochs later at most
+    instead of at the end of the fit, and no further persistent launches run
+    on the uneven position counters a failed sweep leaves."""
+
+    def __init__(self, engine: SGDEngine):
+        self.e = engine
+        self.host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.ev = None
+
+    def post(self) -> None:
+        ws = getattr(self.e, "_strata_ws", None)
+        if ws is None or self.ev is not None and not self.ev.query():
+            return                                # the last copy is still in flight
+        B = self.e.strata.B
+        self.host.copy_(ws[B:B + 1], non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record()
+
+    def failed(self) -> bool:
+        return self.ev is not None and self.ev.query() and int(self.host[0]) != 0
+
+
 def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
                reg: float, update_user: bool = True, update_item: bool = True,
                verbose: int = 0, rng_order: Optional[np.ndarray] = None,
@@ -1267,8 +1379,9 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
     exact:   draws ``np.random.shuffle`` on the row order every epoch
              (the reference's RNG stream, :371);
     colored: draws ``np.random.permutation(n_colours)`` every epoch;
-    strata:  draws ``np.random.permutation(B)`` (stratum order) and a 32-bit
-             colour-rotation seed every epoch.
+    strata:  draws the stratum order (``stratum_order``: np.random.permutation(B)
+             for the plain plan) and a 32-bit colour-rotation seed every
+             epoch.
 
     Strata epochs run back to back with no host synchronisation: the
     persistent sweep's error word is sticky, so it is read only where the
@@ -1289,15 +1402,16 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
     elif schedule == "strata":
         if engine.strata is None:
             engine.prepare_strata()
-        nb = engine.strata.B
     else:
         raise ValueError(f"schedule must be 'exact', 'colored' or 'strata', got {schedule!r}")
     train_rmse = []
     draws = []                                    # strata: (seq, seed) per epoch
     persistent = None                             # strata: the engine's default
     snap0 = None
+    poll = None
     if schedule == "strata" and engine.strata_persistent:
         snap0 = engine.snapshot_params()          # once: the replay's starting point
+        poll = _ErrorPoll(engine)
 
     def replay_failed(upto: int) -> None:
         """Epochs 0..upto-1 again from snap0 as per-stratum launches."""
@@ -1313,6 +1427,8 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
             engine.sse_async(ep)
 
     for epoch in range(n_epochs):
+        if poll is not None and persistent is None and poll.failed():
+            replay_failed(epoch)                  # stop launching persistent sweeps now
         if schedule == "exact":
             _prep.legacy_shuffle_(order)          # = np.random.shuffle(order)
             engine.epoch_exact(order, lr, reg, update_user, update_item)
@@ -1320,11 +1436,13 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
             seq = np.random.permutation(nb).astype(np.int32)
             engine.epoch_colored(seq, lr, reg, update_user, update_item)
         else:
-            seq = stratum_order(np.random, nb)
+            seq = stratum_order(np.random, engine.strata)
             seed = int(np.random.randint(0, 2**31 - 1))
             draws.append((seq, seed))
             engine.epoch_strata(seq, seed, lr, reg, update_user, update_item,
                                 persistent=persistent)
+            if poll is not None and persistent is None:
+                poll.post()
         engine.sse_async(epoch)
         if verbose == 1:
             if snap0 is not None and persistent is None and engine.strata_failed():

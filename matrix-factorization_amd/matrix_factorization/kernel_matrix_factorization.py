@@ -33,6 +33,7 @@ Three keyword arguments are new and default to the reference's behaviour:
 
 from __future__ import annotations
 
+from concurrent.futures import ThreadPoolExecutor
 from typing import Union
 
 import numpy as np
@@ -119,15 +120,24 @@ class KernelMF(RecommenderBase):
         self.exchange = exchange
 
     # ----------------------------------------------------- device state
-    def _make_engine(self, X: pd.DataFrame) -> SGDEngine:
+    def _make_engine(self, X: pd.DataFrame, n_users: int, n_items: int,
+                     schedule: str = None) -> SGDEngine:
+        """Ratings uploaded, evaluation order built and, for ``schedule``
+        "strata" / "colored", the schedule planned (what fit_epochs would
+        otherwise do first)."""
         n = len(X)
         u = X["user_id"].to_numpy(np.int32) if n else np.zeros(0, np.int32)
         i = X["item_id"].to_numpy(np.int32) if n else np.zeros(0, np.int32)
         r = X["rating"].to_numpy(np.float64) if n else np.zeros(0)
-        return SGDEngine(u, i, r, len(self.user_features), len(self.item_features),
-                         self.n_factors, self.kernel, self.dtype, self.device,
-                         gamma=self.gamma, min_rating=self.min_rating,
-                         max_rating=self.max_rating, global_mean=self.global_mean)
+        eng = SGDEngine(u, i, r, n_users, n_items,
+                        self.n_factors, self.kernel, self.dtype, self.device,
+                        gamma=self.gamma, min_rating=self.min_rating,
+                        max_rating=self.max_rating, global_mean=self.global_mean)
+        if schedule == "strata" and n:
+            eng.prepare_strata()
+        elif schedule == "colored" and n:
+            eng.prepare_colored()
+        return eng
 
     def _sync_params(self, eng: SGDEngine) -> None:
         P, Q, bu, bi = eng.params_numpy()
@@ -201,11 +211,22 @@ class KernelMF(RecommenderBase):
         self.global_mean = X["rating"].mean()
         self.user_biases = np.zeros(self.n_users)
         self.item_biases = np.zeros(self.n_items)
-        self.user_features = np.random.normal(self.init_mean, self.init_sd,
-                                              (self.n_users, self.n_factors))
-        self.item_features = np.random.normal(self.init_mean, self.init_sd,
-                                              (self.n_items, self.n_factors))
-        if self.distributed and world_info()[0] > 1:
+        sharded = self.distributed and world_info()[0] > 1
+        fut = None
+        with ThreadPoolExecutor(1) as ex:
+            if not sharded:
+                # the device side (upload, evaluation order, schedule plan)
+                # is built on a worker thread while this one draws the
+                # initial factors: the worker draws nothing, so the RNG
+                # stream is the reference's (sample, normal P, normal Q)
+                fut = ex.submit(self._make_engine, X, self.n_users, self.n_items,
+                                self.schedule)
+            self.user_features = np.random.normal(self.init_mean, self.init_sd,
+                                                  (self.n_users, self.n_factors))
+            self.item_features = np.random.normal(self.init_mean, self.init_sd,
+                                                  (self.n_items, self.n_factors))
+            eng = fut.result() if fut is not None else None
+        if sharded:
             n = len(X)
             P, Q, bu, bi, rmse, _ = fit_sharded(
                 X["user_id"].to_numpy(np.int32), X["item_id"].to_numpy(np.int32),
@@ -221,7 +242,6 @@ class KernelMF(RecommenderBase):
             self.train_rmse = rmse
             self._pred_engine = None
             return self
-        eng = self._make_engine(X)
         eng.load_params(self.user_features, self.item_features,
                         self.user_biases, self.item_biases)
         self.train_rmse = fit_epochs(eng, self.n_epochs, self.schedule, self.lr,
@@ -262,7 +282,9 @@ class KernelMF(RecommenderBase):
                                              (n_new_users, self.n_factors))
         self.user_features = np.concatenate((self.user_features, new_user_features),
                                             axis=0)
-        eng = self._make_engine(X)
+        # n_users is not updated by update_users (the reference's quirk,
+        # :213-235): the engine takes the row counts of the arrays
+        eng = self._make_engine(X, len(self.user_features), len(self.item_features))
         eng.load_params(self.user_features, self.item_features,
                         self.user_biases, self.item_biases)
         self.train_rmse = fit_epochs(eng, n_epochs, self.schedule, lr, self.reg,

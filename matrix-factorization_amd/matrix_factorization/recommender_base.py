@@ -11,6 +11,7 @@ the same calls gives the reference's results.
 from __future__ import annotations
 
 from abc import ABCMeta, abstractmethod
+from concurrent.futures import ThreadPoolExecutor
 from typing import Any, Tuple, Union
 
 import numpy as np
@@ -26,6 +27,20 @@ FAST_PREP_MIN_ROWS = 1 << 16
 
 def _index_of(keys) -> pd.Index:
     return pd.Index(list(keys))
+
+
+def _aligned_rating(X: pd.DataFrame, y):
+    """The values ``X["rating"] = y`` puts in the column (recommender_base.py:
+    123), read without copying the frame: a Series on the same index as is,
+    else reindexed to X's index as the assignment aligns it; None (take the
+    pandas path) for anything that is not a Series."""
+    if not isinstance(y, pd.Series):
+        return None
+    if y.index.equals(X.index):
+        return y.to_numpy()
+    if not X.index.is_unique or not y.index.is_unique:
+        return None
+    return y.reindex(X.index).to_numpy()
 
 
 class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
@@ -81,20 +96,33 @@ class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
                  new users to user_id_map (ids max + 1, ...);
         predict: unknown ids become -1.
         Returns a frame with int64 user_id / item_id (and rating).
+
+        Integer ids of at least FAST_PREP_MIN_ROWS rows take the native path
+        (mf_prep.cpp), same results: the duplicate check runs on worker
+        threads while this thread draws the permutation (the RNG state is
+        put back if the check then raises, so a failed fit draws nothing, as
+        in the reference), and fit reads the id columns and ``y`` in place
+        instead of copying the frame first.
         """
+        native = None
+        if type in ("fit", "update"):
+            ids = self._int64_ids(X)
+            if ids is not None:
+                perm = self._checked_permutation(ids)
+                rating = _aligned_rating(X, y) if type == "fit" else None
+                if rating is not None:
+                    return self._fit_maps_native(X.index, ids, rating, perm)
+                native = perm
+
         X = X.loc[:, ["user_id", "item_id"]]
         if type != "predict":
             X["rating"] = y
 
         if type in ("fit", "update"):
-            ids = self._int64_ids(X)
-            if ids is not None:
-                if _prep.pairs_duplicated(*ids):
-                    raise ValueError("Duplicate user-item ratings in matrix")
-                perm = _prep.legacy_permutation(len(X))       # = X.sample's draw
+            if native is not None:
                 if type == "fit":
-                    return self._fit_maps_native(X, ids, perm)
-                X = X.iloc[perm]
+                    return self._fit_maps_native(X.index, ids, X["rating"].to_numpy(), native)
+                X = X.iloc[native]
             else:
                 if X.duplicated(subset=["user_id", "item_id"]).sum() != 0:
                     raise ValueError("Duplicate user-item ratings in matrix")
@@ -133,34 +161,54 @@ class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
             return out, known_users, new_users
         return out
 
-    @staticmethod
-    def _int64_ids(X: pd.DataFrame):
+    def _int64_ids(self, X: pd.DataFrame):
         """(user ids, item ids) as int64 arrays when both columns are integer
         and the frame is large enough for the native path, else None."""
         if len(X) < FAST_PREP_MIN_ROWS:
             return None
-        u = _prep.as_int64_ids(X["user_id"].to_numpy())
-        i = _prep.as_int64_ids(X["item_id"].to_numpy())
+        cu, ci = X["user_id"], X["item_id"]
+        u = _prep.as_int64_ids(cu.to_numpy())
+        i = _prep.as_int64_ids(ci.to_numpy())
+        self._id_dtypes = (cu.dtype, ci.dtype)
         return None if u is None or i is None else (u, i)
 
-    def _fit_maps_native(self, X: pd.DataFrame, ids, perm: np.ndarray) -> pd.DataFrame:
+    @staticmethod
+    def _checked_permutation(ids) -> np.ndarray:
+        """The duplicate-pair check (recommender_base.py:125-128) on worker
+        threads beside ``X.sample(frac=1)``'s draw (:131) on this one; if the
+        check fails, the RNG state is restored before the ValueError."""
+        state = np.random.get_state()
+        with ThreadPoolExecutor(1) as ex:
+            dup = ex.submit(_prep.pairs_duplicated, *ids)
+            perm = _prep.legacy_permutation(len(ids[0]))       # = X.sample's draw
+            if dup.result():
+                np.random.set_state(state)
+                raise ValueError("Duplicate user-item ratings in matrix")
+        return perm
+
+    def _fit_maps_native(self, index: pd.Index, ids, rating: np.ndarray,
+                         perm: np.ndarray) -> pd.DataFrame:
         """The fit branch for integer ids: the rows in ``perm`` order (the
         order X.sample(frac=1) gives), id maps in first-appearance order of
         that order (pd.factorize / unique of the shuffled column), all in
-        mf_prep.cpp."""
+        mf_prep.cpp (users and items on two threads)."""
+
+        def one(v):
+            c, uniq = _prep.factorize(_prep.gather(v, perm))
+            return c, uniq
+
+        with ThreadPoolExecutor(2) as ex:
+            res = list(ex.map(one, ids))
         maps = []
         codes = []
-        for col, v in zip(("user_id", "item_id"), ids):
-            c, uniq = _prep.factorize(_prep.gather(v, perm))
-            dt = X[col].dtype
+        for (c, uniq), dt in zip(res, self._id_dtypes):
             uniq = uniq.view(dt) if dt.itemsize == 8 else uniq.astype(dt)
             maps.append(dict(zip(uniq, range(len(uniq)))))
             codes.append(c)
         self.user_id_map, self.item_id_map = maps
         self.n_users, self.n_items = len(maps[0]), len(maps[1])
-        rating = X["rating"].to_numpy()
         rating = _prep.gather(rating, perm) if rating.dtype.kind in "fiu" else rating[perm]
-        idx = X.index
+        idx = index
         if isinstance(idx, pd.RangeIndex):
             idx = pd.Index(idx.start + idx.step * perm if (idx.start, idx.step) != (0, 1)
                            else perm)

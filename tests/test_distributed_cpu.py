@@ -79,11 +79,12 @@ class CpuEngine:
         self.colored = offs
         return len(offs) - 1
 
-    def prepare_strata(self, n_blocks=None, item_bounds=None):
+    def prepare_strata(self, n_blocks=None, item_bounds=None, classes=None):
         from matrix_factorization.engine import (PhasedStrata, StrataPlan, balanced_bounds,
                                                  sched_strata, strata_slots)
 
         B = STRATA_B if n_blocks is None else n_blocks
+        C = classes or 1
         if item_bounds is not None:          # the product's PhasedStrata over given ranges
             ilo = np.asarray(item_bounds, np.int64)
             ns = strata_slots(self.k, self.dcode)
@@ -92,19 +93,19 @@ class CpuEngine:
                 ix = np.flatnonzero((self.i_host >= ilo[p]) & (self.i_host < ilo[p + 1]))
                 uu, ii = self.u_host[ix], self.i_host[ix] - int(ilo[p])
                 m = int(ilo[p + 1] - ilo[p])
-                ub = balanced_bounds(uu, self.n_users, B)
+                ub = balanced_bounds(uu, self.n_users, C * B)
                 ib = balanced_bounds(ii, m, B)
-                sched, bstep = sched_strata(uu, ii, self.n_users, m, B, ub, ib, ns)
-                plans.append(StrataPlan(B, ns, ub, ib, bstep, sched))
+                sched, bstep = sched_strata(uu, ii, self.n_users, m, B, ub, ib, ns, C)
+                plans.append(StrataPlan(B, ns, ub, ib, bstep, sched, C))
                 idx.append(ix)
             self.strata = PhasedStrata(plans, idx, ilo)
             return self.strata
-        ub = balanced_bounds(self.u_host, self.n_users, B)
+        ub = balanced_bounds(self.u_host, self.n_users, C * B)
         ib = balanced_bounds(self.i_host, self.n_items, B)
         ns = strata_slots(self.k, self.dcode)
         sched, bstep = sched_strata(self.u_host, self.i_host, self.n_users, self.n_items, B,
-                                    ub, ib, ns)
-        self.strata = StrataPlan(B, ns, ub, ib, bstep, sched)
+                                    ub, ib, ns, C)
+        self.strata = StrataPlan(B, ns, ub, ib, bstep, sched, C)
         return self.strata
 
     def epoch_strata(self, seq, seed, lr, reg, update_user=True, update_item=True,

@@ -389,6 +389,12 @@ def test_l2_handoff_equals_per_stratum_launches(kernel, k, B, waves, monkeypatch
         for ep in range(3):
             seq = stratum_order(np.random.RandomState(ep), B, "xcd")
             eng.epoch_strata(seq, 3000 + ep, lr=0.01, reg=0.02, persistent=persistent)
+            if persistent and ep == 0:
+                # first launch on a freshly zeroed workspace: its tag is 1
+                # (base 0 + 1), never the 0 of an unpublished entry
+                torch.cuda.synchronize()
+                ws = eng._strata_ws.cpu().numpy().view(np.int32)
+                assert np.all(ws[B + 1: 2 * B + 1] >> 4 == 1)
         eng.check_strata()
         if persistent:
             torch.cuda.synchronize()
@@ -426,3 +432,67 @@ def test_contiguous_rows_allocation():
     eng.load_params(P, np.zeros((50, k), np.float32), np.zeros(nu), np.zeros(50))
     assert hasattr(eng.P, "_mf_block")
     assert np.array_equal(eng.P.cpu().numpy(), P)
+
+
+@pytest.mark.parametrize("dtype,kernel,k,B,C,waves,phases", [
+    ("float64", "linear", 64, 4, 2, None, None),
+    ("float64", "sigmoid", 32, 3, 3, None, None),
+    ("float32", "linear", 64, 16, 4, None, None),
+    ("float32", "sigmoid", 32, 8, 2, 8, None),       # 8 waves, rows two steps ahead
+    ("float64", "linear", 64, 4, 2, None, 2),        # item phases
+    ("float64", "rbf", 16, 5, 2, None, None),
+])
+def test_user_range_classes(dtype, kernel, k, B, C, waves, phases):
+    """C user-range classes (C*B user ranges, C*B strata; the persistent
+    kernel waits for the holder C positions back, so every hand-off has C - 1
+    blocks of slack): the persistent epoch is bit-identical to one launch per
+    stratum, the result is the oracle's sweep in plan.serial_order, and an
+    order that does not cycle through the classes runs per stratum (the
+    launcher refuses the persistent form) with the same bits as that order's
+    per-stratum launches."""
+    import oracle
+    from matrix_factorization.engine import stratum_order
+
+    nu, ni, nnz = 3000, 900, 120000
+    u, i, r = _synthetic(91, nu, ni, nnz)
+    rs = np.random.RandomState(92)
+    P0 = rs.normal(0, 0.1, (nu, k)); Q0 = rs.normal(0, 0.1, (ni, k))
+    bu0 = rs.normal(0, 0.1, nu); bi0 = rs.normal(0, 0.1, ni)
+    out = []
+    n_ph = phases or 1
+    for persistent in (True, False):
+        eng = _engine(u, i, r, nu, ni, k, kernel, dtype, P0, Q0, bu0, bi0)
+        plan = eng.prepare_strata(n_blocks=B, waves=waves, phases=phases, classes=C)
+        assert plan.classes == C and plan.n_strata == C * B
+        eps = []
+        for ep in range(3):
+            seq = stratum_order(np.random.RandomState(ep), plan)
+            ms = eng.epoch_strata(seq, 4000 + ep, lr=0.01, reg=0.02, persistent=persistent,
+                                  timing=True)
+            assert ms[1] == (n_ph if persistent else n_ph * C * B)
+            eps.append((seq, 4000 + ep))
+        eng.check_strata()
+        out.append(eng.params_numpy())
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    hyp = dict(kernel=kernel, gamma=1.0 / k, min_rating=1.0, max_rating=5.0)
+    P2, Q2, bu2, bi2 = P0.copy(), Q0.copy(), bu0.copy(), bi0.copy()
+    for seq, seed in eps:
+        order = plan.serial_order(seq, seed)
+        assert np.array_equal(np.sort(order), np.arange(nnz))
+        oracle.sgd_pass(eng.u_host, eng.i_host, eng.r_host.astype(np.float64), eng.global_mean,
+                        bu2, bi2, P2, Q2, lr=0.01, reg=0.02, order=order, **hyp)
+    tol = 1e-11 if dtype == "float64" else 1e-4
+    for g, o in zip(out[0], (P2, Q2, bu2, bi2)):
+        _close(g, o, tol)
+    # classes not dealt round-robin (all of class 0 first): per-stratum launches
+    bad = np.concatenate([np.arange(c, C * B, C) for c in range(C)]).astype(np.int32)
+    res = []
+    for persistent in (True, False):
+        eng = _engine(u, i, r, nu, ni, k, kernel, dtype, P0, Q0, bu0, bi0)
+        eng.prepare_strata(n_blocks=B, waves=waves, phases=phases, classes=C)
+        ms = eng.epoch_strata(bad, 7, lr=0.01, reg=0.02, persistent=persistent, timing=True)
+        assert ms[1] == n_ph * C * B
+        res.append(eng.params_numpy())
+    for a, b in zip(*res):
+        assert np.array_equal(a, b)

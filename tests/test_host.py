@@ -363,10 +363,12 @@ def test_slice_order_groups_items_then_users():
 
 
 # ------------------------------------------------------------ strata plan
-@pytest.mark.parametrize("B,NS", [(1, 32), (3, 16), (8, 128)])
-def test_strata_plan_is_valid(B, NS):
-    """mf_strata_plan_build: every rating placed once; block (s, w) holds user
-    range (w+s)%B x item range w; a step holds each slot and each item at most
+@pytest.mark.parametrize("B,NS,C", [(1, 32, 1), (3, 16, 1), (8, 128, 1), (1, 32, 2),
+                                    (3, 16, 2), (8, 64, 3), (5, 32, 4)])
+def test_strata_plan_is_valid(B, NS, C):
+    """mf_strata_plan_build_classes: every rating placed once; block (s, w),
+    s < C*B, holds user range (s + C*w) mod C*B x item range w (C = 1: the
+    plain plan, (w+s) mod B); a step holds each slot and each item at most
     once; every user of a block stays on one slot; the block has exactly
     D = max(slot load, item degree) steps (Koenig colouring)."""
     from matrix_factorization import engine as E
@@ -376,18 +378,20 @@ def test_strata_plan_is_valid(B, NS):
     keys = rs.choice(nu * ni, n, replace=False)
     u = (keys // ni).astype(np.int32)
     i = (keys % ni).astype(np.int32)
-    ub = E.balanced_bounds(u, nu, B)
+    ub = E.balanced_bounds(u, nu, C * B)
     ib = E.balanced_bounds(i, ni, B)
-    sched, bstep = E.sched_strata(u, i, nu, ni, B, ub, ib, NS)
+    sched, bstep = E.sched_strata(u, i, nu, ni, B, ub, ib, NS, C)
+    assert len(bstep) == C * B * B + 1
     assert len(sched) == bstep[-1] * NS
     valid = sched[sched >= 0]
     assert np.array_equal(np.sort(valid), np.arange(n))
-    for s in range(B):
+    for s in range(C * B):
         for w in range(B):
             blk = s * B + w
             nst = bstep[blk + 1] - bstep[blk]
             grid = sched[bstep[blk] * NS:bstep[blk + 1] * NS].reshape(nst, NS)
-            ubk = (w + s) % B
+            ubk = (s + C * w) % (C * B)
+            assert ubk % C == s % C                 # stratum s: class s mod C only
             js = grid[grid >= 0]
             assert np.all((u[js] >= ub[ubk]) & (u[js] < ub[ubk + 1]))
             assert np.all((i[js] >= ib[w]) & (i[js] < ib[w + 1]))
@@ -436,6 +440,40 @@ def test_strata_serial_order_and_rejections():
     assert E.strata_slots(16, _lib.MF_F32) == 256
     assert E.strata_slots(64, _lib.MF_F64) == 64          # one slot per group (FP64 rows)
     assert _lib.load().mf_strata_slots(-1, 0) == -1
+
+
+@pytest.mark.parametrize("C", [1, 2, 3, 4])
+def test_stratum_order_cycles_classes(C):
+    """stratum_order with C user-range classes: a permutation of the C*B
+    strata that deals the classes round-robin (what the persistent kernel's
+    C-positions-back wait needs: a user range is used again exactly C
+    positions later); C = 1 draws exactly rs.permutation(B), as before."""
+    from types import SimpleNamespace
+
+    from matrix_factorization.engine import stratum_order
+
+    B = 7
+    seq = stratum_order(np.random.RandomState(3), SimpleNamespace(B=B, classes=C))
+    assert seq.dtype == np.int32 and np.array_equal(np.sort(seq), np.arange(C * B))
+    cls = seq % C
+    assert len(set(cls[:C])) == C
+    assert np.all(cls == cls[np.arange(C * B) % C])
+    if C == 1:
+        assert np.array_equal(seq, np.random.RandomState(3).permutation(B))
+    # the serial order of a classes plan: every rating once, stratum by stratum
+    from matrix_factorization import engine as E
+
+    rs = np.random.RandomState(1)
+    nu, ni, n = 400, 90, 4000
+    keys = rs.choice(nu * ni, n, replace=False)
+    u = (keys // ni).astype(np.int32)
+    i = (keys % ni).astype(np.int32)
+    ub, ib = E.balanced_bounds(u, nu, C * B), E.balanced_bounds(i, ni, B)
+    sched, bstep = E.sched_strata(u, i, nu, ni, B, ub, ib, 16, C)
+    plan = E.StrataPlan(B, 16, ub, ib, bstep, sched, C)
+    assert plan.n_strata == C * B and len(plan.stratum_sizes()) == C * B
+    order = plan.serial_order(seq, 99)
+    assert np.array_equal(np.sort(order), np.arange(n))
 
 
 def test_phased_strata_host_composition():

@@ -159,7 +159,37 @@ def test_duplicates_raise(fast, monkeypatch):
     st = np.random.get_state()
     with pytest.raises(ValueError, match="Duplicate"):
         _run(KernelMF(), X, y, "fit", fast, monkeypatch, 0)
+    # the check fails before X.sample's draw: the RNG is where seed(0) left it
+    after = np.random.get_state()
+    np.random.seed(0)
+    assert _state_equal(after, np.random.get_state())
     np.random.set_state(st)
+
+
+@pytest.mark.parametrize("ykind", ["permuted_index", "int_series", "array", "partial_index"])
+def test_fit_preprocess_rating_alignment(ykind, monkeypatch):
+    """X["rating"] = y aligns a Series on X's index (and takes an array as
+    it stands): the native path, which reads y in place, gives the frame
+    the pandas path gives for each form of y."""
+    n = 12_000
+    X, y = _frame(n, np.int64, 6, pd.Index(np.arange(n) * 3 + 2))
+    rs = np.random.RandomState(9)
+    if ykind == "permuted_index":
+        y = y.iloc[rs.permutation(n)]
+    elif ykind == "int_series":
+        y = y.astype(np.int64)
+    elif ykind == "array":
+        y = y.to_numpy()
+    else:
+        y = y.iloc[: n - 100].copy()
+        y.index = y.index + 1                      # some labels missing: NaN ratings
+    ma, mb = KernelMF(), KernelMF()
+    a, sa = _run(ma, X, y, "fit", True, monkeypatch, 4)
+    b, sb = _run(mb, X, y, "fit", False, monkeypatch, 4)
+    assert _state_equal(sa, sb) and a.index.equals(b.index)
+    for c in ("user_id", "item_id", "rating"):
+        assert a[c].dtype == b[c].dtype
+        assert np.array_equal(a[c].to_numpy(), b[c].to_numpy(), equal_nan=True)
 
 
 def test_update_preprocess_native_equals_pandas(monkeypatch):

@@ -15,7 +15,8 @@
 #   pmc:CTRS[:ARGS]      rocprofv3 --pmc CTRS (+ kernel trace) -- python bench.py ARGS
 #                        (CTRS '+'-separated; one pass, within the per-block limits)
 #   calib                FETCH_SIZE / WRITE_SIZE passes over tools/calib_fetch
-#   py:SCRIPT[:ARGS]     python SCRIPT ARGS              (probes under tools/)
+#   py:SCRIPT[:ARGS]     python SCRIPT ARGS              (probes under tools/; limit
+#                        $PY_TIMEOUT s, default 600 -- set it with env:PY_TIMEOUT=N)
 #   dist:N[:ARGS]        torch.distributed.run N gloo ranks on this one GPU:
 #                        python bench.py --gpus N --backend gloo ARGS
 #   env:VAR=VAL          export VAR=VAL for the following steps (VAL empty: unset)
@@ -62,7 +63,7 @@ for step in "$@"; do
         script=${rest%%:*}
         pargs=""
         [[ "$rest" == *:* ]] && pargs=${rest#*:}
-        timeout -k 10 600 python -u "$script" ${pargs//,/ } > "$p.out" 2> "$p.log" ;;
+        timeout -k 10 ${PY_TIMEOUT:-600} python -u "$script" ${pargs//,/ } > "$p.out" 2> "$p.log" ;;
     dist)
         nr=${rest%%:*}
         dargs=""

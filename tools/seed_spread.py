@@ -37,7 +37,59 @@ def log(msg):
     print(f"[seed_spread {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def summarize(runs):
+    """Per family and epoch: mean, sample SD, standard error of the mean; per
+    non-reference family the difference of means to the reference order
+    ("exact") with its standard error sqrt(se_a^2 + se_b^2)."""
+    fam = {}
+    for run in runs:
+        fam.setdefault(run["family"], []).append(run["rmse"])
+    stats = {}
+    for f, v in fam.items():
+        a = np.asarray(v, dtype=np.float64)                 # runs x epochs
+        n = a.shape[0]
+        sd = a.std(axis=0, ddof=1) if n > 1 else np.full(a.shape[1], np.nan)
+        stats[f] = {"n": n, "mean": a.mean(axis=0).tolist(), "sd": sd.tolist(),
+                    "se": (sd / np.sqrt(n)).tolist()}
+    diff = {}
+    if "exact" in stats:
+        ref = stats["exact"]
+        for f, st in stats.items():
+            if f == "exact":
+                continue
+            d = np.asarray(st["mean"]) - np.asarray(ref["mean"])
+            se = np.sqrt(np.asarray(st["se"]) ** 2 + np.asarray(ref["se"]) ** 2)
+            diff[f] = {"minus_exact": d.tolist(), "se": se.tolist(),
+                       "z": (d / se).tolist()}
+    final = {f: {"n": st["n"], "mean_final": st["mean"][-1], "sd_final": st["sd"][-1],
+                 "se_final": st["se"][-1],
+                 "finals": [r[-1] for r in fam[f]],
+                 "spread_final": float(np.max([r[-1] for r in fam[f]]) -
+                                       np.min([r[-1] for r in fam[f]]))}
+             for f, st in stats.items()}
+    for f, d in diff.items():
+        final[f].update(minus_exact=d["minus_exact"][-1], se_diff=d["se"][-1],
+                        z=d["z"][-1])
+    return {"final": final, "per_epoch": stats, "vs_exact": diff}
+
+
+def merge(paths, out):
+    """Combine the runs of several seed_spread outputs (same workload, epochs)."""
+    runs, head = [], None
+    for p in paths:
+        with open(p) as f:
+            d = json.load(f)
+        head = head or {k: d[k] for k in ("workload", "epochs", "lr", "reg")}
+        runs += d["runs"]
+    doc = dict(head, summary=summarize(runs), runs=runs, merged_from=paths)
+    with open(out, "w") as f:
+        json.dump(doc, f)
+    print(json.dumps(doc["summary"]["final"], indent=1))
+
+
 def main():
+    if len(sys.argv) > 2 and sys.argv[1] == "--merge":
+        return merge(sys.argv[3:], sys.argv[2])
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--epochs", type=int, default=20)
@@ -47,6 +99,11 @@ def main():
     ap.add_argument("--lr", type=float, default=0.01)
     ap.add_argument("--reg", type=float, default=0.02)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--variants", nargs="*", default=["C1"],
+                    help="strata plan variants: C<n> = n user-range classes, B<n> = n "
+                         "blocks, joined with '_' (C2_B128); family strata_<variant> "
+                         "(C1: family 'strata')")
     args = ap.parse_args()
 
     import torch
@@ -69,7 +126,7 @@ def main():
     runs = []
 
     def fresh():
-        e = SGDEngine(u, i, r, nu, ni, k, kernel, "float32", dev, **hyp)
+        e = SGDEngine(u, i, r, nu, ni, k, kernel, args.dtype, dev, **hyp)
         e.load_params(P=P0, Q=Q0, bu=np.zeros(nu), bi=np.zeros(ni))
         return e
 
@@ -85,24 +142,31 @@ def main():
             if ep % 5 == 4:
                 log(f"exact seed {s}: epoch {ep + 1}/{E} ({time.time() - t0:.0f}s)")
         rm = e.rmse_values(E)
-        runs.append({"family": "exact", "seed": s, "rmse": rm, "s": time.time() - t0})
+        runs.append({"family": "exact", "seed": s, "rmse": rm, "s": time.time() - t0,
+                     "dtype": args.dtype})
         log(f"exact seed {s}: final {rm[-1]:.7f} in {time.time() - t0:.0f}s")
         del e
         torch.cuda.empty_cache()
 
-    for s in args.draw_seeds:
-        e = fresh()
-        pl = e.prepare_strata()
-        for ep in range(E):
-            rsd = np.random.RandomState([s, ep])
-            e.epoch_strata(stratum_order(rsd, pl.B),
-                           int(rsd.randint(0, 2**31 - 1)), args.lr, args.reg)
-            e.sse_async(ep)
-        rm = e.rmse_values(E)
-        runs.append({"family": "strata", "seed": s, "rmse": rm})
-        log(f"strata seed {s}: final {rm[-1]:.7f}")
-        del e
-        torch.cuda.empty_cache()
+    for var in args.variants:
+        opt = {"C": 1, "B": None}
+        for part in var.split("_"):
+            opt[part[0]] = int(part[1:])
+        fam = "strata" if var == "C1" else f"strata_{var}"
+        for s in args.draw_seeds:
+            e = fresh()
+            pl = e.prepare_strata(n_blocks=opt["B"], classes=opt["C"])
+            for ep in range(E):
+                rsd = np.random.RandomState([s, ep])
+                e.epoch_strata(stratum_order(rsd, pl),
+                               int(rsd.randint(0, 2**31 - 1)), args.lr, args.reg)
+                e.sse_async(ep)
+            rm = e.rmse_values(E)
+            runs.append({"family": fam, "seed": s, "rmse": rm, "dtype": args.dtype,
+                         "B": pl.B, "classes": pl.classes})
+            log(f"{fam} (B={pl.B}, C={pl.classes}) seed {s}: final {rm[-1]:.7f}")
+            del e
+            torch.cuda.empty_cache()
 
     for W in args.worlds:
         rp = RotationReplay(u, i, r, nu, ni, W, k, kernel, "float32", dev, **hyp)
@@ -118,20 +182,14 @@ def main():
         del rp
         torch.cuda.empty_cache()
 
-    fam = {}
-    for run in runs:
-        fam.setdefault(run["family"], []).append(run["rmse"][-1])
-    summary = {f: {"n": len(v), "mean_final": float(np.mean(v)),
-                   "spread_final": float(np.max(v) - np.min(v)), "finals": v}
-               for f, v in fam.items()}
     doc = {"workload": desc, "epochs": E, "lr": args.lr, "reg": args.reg,
-           "summary": summary, "runs": runs}
+           "summary": summarize(runs), "runs": runs}
     txt = json.dumps(doc)
     if args.out:
         with open(args.out, "w") as f:
             f.write(txt)
     print(txt)
-    log(json.dumps(summary))
+    log(json.dumps(doc["summary"]["final"]))
 
 
 if __name__ == "__main__":

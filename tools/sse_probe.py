@@ -24,12 +24,13 @@ def main():
     import matrix_factorization.engine as E
     E.N_SLICES = int(os.environ.get("SSE_PROBE_SLICES", E.N_SLICES))   # evaluation slices
     u, i, r = bench.synth(nu, ni, nnz)
-    eng = SGDEngine(u, i, r, nu, ni, k, "linear", "float32", "cuda:0",
+    dt = os.environ.get("SSE_PROBE_DTYPE", "float32")
+    eng = SGDEngine(u, i, r, nu, ni, k, "linear", dt, "cuda:0",
                     global_mean=float(r.mean()), min_rating=1, max_rating=5)
     rs = np.random.RandomState(0)
-    eng.load_params(rs.normal(0, 0.1, (nu, k)).astype(np.float32),
-                    rs.normal(0, 0.1, (ni, k)).astype(np.float32),
-                    np.zeros(nu, np.float32), np.zeros(ni, np.float32))
+    eng.load_params(rs.normal(0, 0.1, (nu, k)).astype(dt),
+                    rs.normal(0, 0.1, (ni, k)).astype(dt),
+                    np.zeros(nu, dt), np.zeros(ni, dt))
     ref = None
     for var, g in runs:
         for key, val in (("MF_SSE_VARIANT", var), ("MF_SSE_BLOCKS", g)):
@@ -51,7 +52,7 @@ def main():
         ms = t0.elapsed_time(t1) / reps
         sse = eng.sse_values(1)[0]
         ref = sse if ref is None else ref
-        print(f"slices={E.N_SLICES} variant={var} blocks={g or 'default'} sse_ms={ms:.3f} sse={sse:.6f} "
+        print(f"dtype={dt} slices={E.N_SLICES} variant={var} blocks={g or 'default'} sse_ms={ms:.3f} sse={sse:.6f} "
               f"rel_to_first={abs(sse - ref) / ref:.2e}", flush=True)
 
 

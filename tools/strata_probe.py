@@ -55,14 +55,14 @@ def main():
             eng.epoch_strata(seq, seed, 0.01, 0.02)
 
     for ep in range(2):
-        run(stratum_order(rs, B), ep)
+        run(stratum_order(rs, plan), ep)
     torch.cuda.synchronize()
     probe = torch.zeros(4 * B * B, dtype=torch.int64, device="cuda:0")
     _lib.call("mf_strata_set_probe", ctypes.c_void_p(probe.data_ptr()))
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
     t0.record()
-    run(stratum_order(rs, B), 7)
+    run(stratum_order(rs, plan), 7)
     t1.record()
     torch.cuda.synchronize()
     _lib.call("mf_strata_set_probe", None)
