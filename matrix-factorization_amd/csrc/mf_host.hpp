@@ -7,8 +7,11 @@
 #include <cstdint>
 #include <cstdlib>
 #include <functional>
+#include <memory>
 #include <thread>
 #include <vector>
+
+#include <sys/mman.h>
 
 namespace mf {
 
@@ -34,6 +37,30 @@ inline void parallel_chunks(int64_t n, int T, const std::function<void(int, int6
         th.emplace_back(fn, t, lo, hi);
     }
     for (auto& x : th) x.join();
+}
+
+// Large host scratch buffers (10^8 entries at C3): anonymous mappings with
+// transparent huge pages requested, not value-initialised -- the threads that
+// fill them touch their pages first, 2 MB at a time where the kernel grants
+// huge pages (a fresh 4 KB-page buffer costs one page fault per 4 KB, and a
+// fit() builds several GB of them).
+struct MapFree {
+    size_t bytes = 0;
+    void operator()(void* p) const {
+        if (p) munmap(p, bytes);
+    }
+};
+template <class T>
+using big_ptr = std::unique_ptr<T[], MapFree>;
+template <class T>
+big_ptr<T> big_alloc(int64_t n) {
+    const size_t bytes = std::max<size_t>(1, (size_t)n * sizeof(T));
+    void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (p == MAP_FAILED) return big_ptr<T>(nullptr, MapFree{0});
+#ifdef MADV_HUGEPAGE
+    (void)madvise(p, bytes, MADV_HUGEPAGE);
+#endif
+    return big_ptr<T>(static_cast<T*>(p), MapFree{bytes});
 }
 
 inline int bucket_bits(int64_t n) {  // 2^R buckets of <= ~16K entries

@@ -41,6 +41,9 @@ void set_error(const char* fmt, ...);
 using mf::bucket_bits;
 using mf::for_buckets;
 using mf::host_threads;
+using mf::big_alloc;
+using mf::big_ptr;
+using mf::MapFree;
 using mf::mix64;
 using mf::parallel_chunks;
 using mf::partition_rows;
@@ -157,9 +160,10 @@ extern "C" int mf_pairs_duplicated(const int64_t* a, const int64_t* b, int64_t n
         return (int)(mix64((uint64_t)a[p] * 0x9E3779B97F4A7C15ull ^ (uint64_t)b[p]) >> (64 - R));
     };
     std::vector<int64_t> start;
-    std::unique_ptr<std::pair<int64_t, int64_t>[]> pr;
+    big_ptr<std::pair<int64_t, int64_t>> pr{nullptr, MapFree{0}};
     try {
-        pr.reset(new std::pair<int64_t, int64_t>[(size_t)n]);
+        pr = big_alloc<std::pair<int64_t, int64_t>>(n);
+        if (!pr) throw std::bad_alloc();
         partition_rows(n, 1 << R, T, bucket, start,
                        [&](int64_t d, int64_t p) { pr[(size_t)d] = {a[p], b[p]}; });
     } catch (const std::bad_alloc&) {
@@ -209,14 +213,15 @@ extern "C" int mf_factorize(const int64_t* vals, int64_t n, int64_t* codes, int6
     auto bucket = [&](int64_t p) { return (int)(mix64((uint64_t)vals[p]) >> (64 - R)); };
     const int64_t nw = (n + 63) >> 6;
     // uninitialised (first touched by the threads that fill them)
-    std::unique_ptr<int64_t[]> slot, sval, lid;
+    big_ptr<int64_t> slot{nullptr, MapFree{0}}, sval{nullptr, MapFree{0}}, lid{nullptr, MapFree{0}};
     std::vector<int64_t> start, wpre;
     std::vector<std::vector<int64_t>> first((size_t)NB);
     std::unique_ptr<std::atomic<uint64_t>[]> bits;
     try {
-        slot.reset(new int64_t[(size_t)n]);
-        sval.reset(new int64_t[(size_t)n]);
-        lid.reset(new int64_t[(size_t)n]);
+        slot = big_alloc<int64_t>(n);
+        sval = big_alloc<int64_t>(n);
+        lid = big_alloc<int64_t>(n);
+        if (!slot || !sval || !lid) throw std::bad_alloc();
         partition_rows(n, 1 << R, T, bucket, start, [&](int64_t d, int64_t p) {
             slot[d] = p;
             sval[d] = vals[p];

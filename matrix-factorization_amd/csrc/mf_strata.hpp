@@ -834,13 +834,14 @@ inline bool strata_coresident(const void* kfn, int B, size_t lds, int threads) {
 
 // NS of the row layout (W, GS, V) that dispatch_rows picks for (k, dtype)
 // Workgroup sizes of the strata kernels: 16 waves (the default), and 8 waves
-// (FP32 only) for plans whose blocks are bound by the item degree rather
-// than by the slot count -- half the slots per step, half the per-step VALU
-// of a CU, about the same number of steps (C2: DESIGN.md section 5).
-// the 8-wave kernels exist for FP32 rows of one vector per lane (k <= 64)
+// for plans whose blocks are bound by the item degree rather than by the slot
+// count -- half the slots per step, half the per-step VALU of a CU, about the
+// same number of steps (C2: DESIGN.md section 5).  The 8-wave kernels exist
+// for rows of one vector per lane (FP32 k <= 64, FP64 k <= 32; FP64 since
+// round 4: C2 in FP64 filled 54 % of the 16-wave plan's slots).
 template <typename T, int V>
 constexpr bool strata_has_8_waves() {
-    return std::is_same<T, float>::value && V == 1;
+    return V == 1;
 }
 
 // the narrow form (MF_FLAG_NARROW): 4 waves whose lane groups are half as
@@ -851,7 +852,8 @@ constexpr bool strata_has_8_waves() {
 // count matches (k <= 32 here).
 template <typename T, int W, int GS, int V>
 constexpr bool strata_has_narrow() {
-    if constexpr (!strata_has_8_waves<T, V>() || GS < 2) return false;
+    if constexpr (!std::is_same<T, float>::value || !strata_has_8_waves<T, V>() || GS < 2)
+        return false;
     else return strata_slots<T, W, GS / 2, 2 * V, 4>() == strata_slots<T, W, GS, V, 8>();
 }
 

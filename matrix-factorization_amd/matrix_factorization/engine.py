@@ -167,6 +167,7 @@ class StrataPlan:
     slots (``sched``: rating index per position, -1 = idle slot)."""
 
     narrow = False      # built for the narrow 4-wave kernels (MF_FLAG_NARROW)
+    l2_handoff = False  # run with MF_FLAG_L2_HANDOFF (chosen by prepare_strata)
 
     def __init__(self, B, NS, ubnd, ibnd, bstep, sched, classes=1):
         self.B, self.NS = int(B), int(NS)
@@ -217,6 +218,10 @@ class StrataPlan:
         cnt = np.concatenate([[0], np.cumsum(self.sched >= 0)])
         edges = self.bstep[:: self.B] * self.NS
         return np.diff(cnt[edges])
+
+    # stratum order of the plan's epochs (stratum_order mode): "xcd" for
+    # plans run with the L2 hand-off, None = the default (MF_STRATA_ORDER)
+    order: Optional[str] = None
 
     def serial_order(self, seq, seed) -> np.ndarray:
         """Rating indices in the order one epoch (strata ``seq``, ``seed``)
@@ -354,6 +359,13 @@ def choose_strata_blocks(u, i, n_users, n_items, k, dcode, max_blocks=None,
 
 
 XCD_CLASSES = 8                  # gfx950: workgroups dealt round-robin over 8 XCDs
+# MF_FLAG_L2_HANDOFF is chosen automatically (with the XCD-class stratum order
+# and B a multiple of 8) when the user rows handed over inside an XCD can stay
+# in its 4 MiB L2: P of at most this many bytes (the B/8 ranges an XCD holds
+# at a time = P/8).  C2 (100K x 32 FP32 = 12.8 MB): SGD 0.943 -> 0.876 ms
+# (B = 69 random order vs B = 72 XCD order + L2, same box);
+# C3 / the N = 8 rotation (P 256 / 32 MB): no gain, not chosen.
+L2_HANDOFF_P_BYTES = 24 << 20
 
 
 class _HipBlock:
@@ -430,6 +442,7 @@ def stratum_order(rs, nb, mode: Optional[str] = None, classes: Optional[int] = N
     """
     if hasattr(nb, "B"):
         classes = nb.classes if classes is None else classes
+        mode = mode or getattr(nb, "order", None)
         nb = nb.B
     classes = int(classes or 1)
     if classes > 1:
@@ -672,16 +685,48 @@ class SGDEngine:
         if phases is None and os.environ.get("MF_STRATA_PHASES"):
             phases = int(os.environ["MF_STRATA_PHASES"])
         bounds = None
+        auto_l2 = False
         if phases is None and n_blocks is None:
             phases, n_blocks, bounds = self._item_phases(classes)
+            if phases == 1 and classes == 1 and self._l2_handoff_fits():
+                B8 = min(self._cus(), -(-n_blocks // XCD_CLASSES) * XCD_CLASSES)
+                b8 = self._bounds_for(B8) if B8 >= 2 * XCD_CLASSES else None
+                if b8 is not None:
+                    n_blocks, bounds, auto_l2 = B8, b8, True
         if phases is not None and int(phases) > 1:
             plan = self._prepare_phased(int(phases), n_blocks, waves, classes=classes)
         else:
             plan = self._build_plan(self.u_host, self.i_host, self.n_items, n_blocks, waves,
                                     bounds, classes)
             plan.to_device(self.u, self.i, self.r, self.dev)
+            if auto_l2:
+                plan.l2_handoff, plan.order = True, "xcd"
         self.strata = plan
         return plan
+
+    def _l2_handoff_fits(self) -> bool:
+        """MF_FLAG_L2_HANDOFF by the plan (env MF_STRATA_L2=0 / 1 forces it
+        off / leaves it to the order): P small enough that the rows an XCD
+        hands over stay in its L2, rows of whole 128-B lines."""
+        if os.environ.get("MF_STRATA_L2") in ("0", "1") or self.bias_only:
+            return False
+        ts = np.dtype(self.ndt).itemsize
+        return (self.n_users * self.k * ts <= L2_HANDOFF_P_BYTES
+                and (self.k * ts) % 128 == 0)
+
+    def _bounds_for(self, B: int):
+        """User / item bounds of a B-block plan over all ratings, or None if
+        its largest block does not fit the LDS."""
+        lib = _lib.load()
+        ub = balanced_bounds(self.u_host, self.n_users, B, cum=self.degree_cum("user"))
+        icum = self.degree_cum("item")
+        for by_count in (True, False):
+            ib = balanced_bounds(self.i_host, self.n_items, B, by_count, cum=icum)
+            need = lib.mf_strata_lds_bytes(int(np.diff(ib).max()), int(np.diff(ub).max()),
+                                           self.k, self.dcode)
+            if need <= lib.mf_strata_lds_limit():
+                return ub, ib
+        return None
 
     def degree_cum(self, side: str) -> Optional[np.ndarray]:
         """Cumulative rating count per user (or item) id, from a histogram of
@@ -709,31 +754,46 @@ class SGDEngine:
                                          cums=(self.degree_cum("user"), self.degree_cum("item")))
         if B <= cus or self.n == 0:
             return 1, B, (ub, ib)
+        icum = self.degree_cum("item")
         for P in range(2, 9):
-            ilo = balanced_bounds(self.i_host, self.n_items, P)
+            ilo = balanced_bounds(self.i_host, self.n_items, P, cum=icum)
             Bp = 0
             for p in range(P):
-                m = (self.i_host >= ilo[p]) & (self.i_host < ilo[p + 1])
-                b, _, _ = choose_strata_blocks(self.u_host[m], self.i_host[m] - ilo[p],
-                                               self.n_users, int(ilo[p + 1] - ilo[p]),
+                # the phase's degree counts on the device; the host arrays are
+                # only sized stand-ins (choose_strata_blocks reads their
+                # lengths when given the counts)
+                lo, hi = int(ilo[p]), int(ilo[p + 1])
+                m = (self.i >= lo) & (self.i < hi)
+                n_p = int(m.sum())
+                cu = torch.cumsum(torch.bincount(self.u[m], minlength=self.n_users),
+                                  0).cpu().numpy()
+                ci = torch.cumsum(torch.bincount(self.i[m] - lo, minlength=max(hi - lo, 1)),
+                                  0).cpu().numpy()
+                del m
+                stand_in = np.empty(n_p, np.int32)
+                b, _, _ = choose_strata_blocks(stand_in, stand_in, self.n_users, hi - lo,
                                                self.k, self.dcode, max_blocks=cus,
-                                               classes=classes)
+                                               classes=classes, cums=(cu, ci))
                 Bp = max(Bp, b)
             if Bp <= cus:
-                return P, Bp, None
+                # every phase on all the CUs: B = CUs fits (the LDS image only
+                # shrinks as B grows) and is faster than the ratings rule's B
+                # (C3 FP64, 2 phases: B = 220 / 240 / 256 -> SGD 21.25 /
+                # 20.49 / 19.99 ms, profiles/r04/classes_probe_fp64_blocks_r04d.txt)
+                return P, max(Bp, min(cus, 256)), None
         return 1, B, (ub, ib)               # no persistent form: one launch per stratum
 
     def _build_plan(self, u, i, n_items, n_blocks, waves, bounds=None,
-                    classes: int = 1) -> "StrataPlan":
+                    classes: int = 1, cums=(None, None)) -> "StrataPlan":
         if bounds is not None:
             B, (ub, ib) = int(n_blocks), bounds
         elif n_blocks is None:
             B, ub, ib = choose_strata_blocks(u, i, self.n_users, n_items, self.k, self.dcode,
-                                             classes=classes)
+                                             classes=classes, cums=cums)
         else:
             B = int(n_blocks)
-            ub = balanced_bounds(u, self.n_users, classes * B)
-            ib = balanced_bounds(i, n_items, B)
+            ub = balanced_bounds(u, self.n_users, classes * B, cum=cums[0])
+            ib = balanced_bounds(i, n_items, B, cum=cums[1])
             need = _lib.load().mf_strata_lds_bytes(int(np.diff(ib).max()), int(np.diff(ub).max()),
                                                    self.k, self.dcode)
             if need > _lib.load().mf_strata_lds_limit():
@@ -762,26 +822,40 @@ class SGDEngine:
     def _prepare_phased(self, P: int, n_blocks, waves, ilo=None,
                         per_b2: float = STRATA_PER_B2, classes: int = 1) -> PhasedStrata:
         if ilo is None:
-            ilo = balanced_bounds(self.i_host, self.n_items, P).astype(np.int64)
-        # one pass over the ratings: each phase's indices in rating order
-        ph = np.searchsorted(ilo[1:], self.i_host, side="right")
-        order = np.argsort(ph, kind="stable")
-        cuts = np.searchsorted(ph[order], np.arange(P + 1))
-        idx = [order[cuts[p]:cuts[p + 1]] for p in range(P)]
+            ilo = balanced_bounds(self.i_host, self.n_items, P,
+                                  cum=self.degree_cum("item")).astype(np.int64)
+        # each phase's rating indices in rating order, found on the device
+        # (10^8 ratings: a host argsort took seconds)
+        bnd = torch.from_numpy(np.ascontiguousarray(ilo[1:-1])).to(self.dev, torch.int32)
+        ph = torch.bucketize(self.i, bnd, right=True)
+        idx_d = [torch.nonzero(ph == p).flatten() for p in range(P)]
+        del ph
+        idx = [t.cpu().numpy() for t in idx_d]
+
+        def cums(p):
+            t = idx_d[p]
+            cu = torch.cumsum(torch.bincount(self.u.index_select(0, t), minlength=self.n_users),
+                              0).cpu().numpy()
+            ci = torch.cumsum(torch.bincount(self.i.index_select(0, t) - int(ilo[p]),
+                                             minlength=max(int(ilo[p + 1] - ilo[p]), 1)),
+                              0).cpu().numpy()
+            return cu, ci
+
+        pcums = [cums(p) for p in range(P)]
         if n_blocks is None:                # one B for every phase: the largest needed
             n_blocks = max(choose_strata_blocks(self.u_host[ix], self.i_host[ix] - ilo[p],
                                                 self.n_users, max(int(ilo[p + 1] - ilo[p]), 1),
                                                 self.k, self.dcode, per_b2=per_b2,
-                                                classes=classes)[0]
+                                                classes=classes, cums=pcums[p])[0]
                            for p, ix in enumerate(idx))
         plans = []
         for p, ix in enumerate(idx):
             ui, ii = self.u_host[ix], self.i_host[ix] - int(ilo[p])
             pl = self._build_plan(ui, ii, int(ilo[p + 1] - ilo[p]), n_blocks, waves,
-                                  classes=classes)
+                                  classes=classes, cums=pcums[p])
             if waves is None:               # phase 0 picks the kernel shape for all
                 waves = 16 if pl.NS == strata_slots(self.k, self.dcode, 16) else 8
-            t = torch.from_numpy(ix).to(self.dev)
+            t = idx_d[p]
             pl.to_device(self.u.index_select(0, t), self.i.index_select(0, t) - int(ilo[p]),
                          self.r.index_select(0, t), self.dev)
             plans.append(pl)
@@ -847,7 +921,8 @@ class SGDEngine:
         # user rows handed over inside an XCD through its L2 (needs the
         # XCD-class stratum order; the launcher checks the order, the kernel
         # the placement) -- DESIGN.md section 5
-        if persistent and os.environ.get("MF_STRATA_L2") == "1":
+        l2 = os.environ.get("MF_STRATA_L2")
+        if persistent and (l2 == "1" or (l2 is None and getattr(pl, "l2_handoff", False))):
             flags |= _lib.MF_FLAG_L2_HANDOFF
         return flags
 

@@ -47,6 +47,13 @@ def test_bench_two_ranks_checks_itself(exchange):
         assert m["replay"]["bit_equal"]
         assert d["phases"]["ring_pass_ms_per_epoch"] > 0
     assert d["roofline"]["frac"] > 0
+    # the default line: FP64 (the reference's arithmetic) at top level, the
+    # FP32 perf layout nested with its own checks
+    assert d["dtype"] == "f64"
+    f = d["fp32_layout"]
+    assert f["dtype"] == "f32" and f["value"] > 0 and f["multi_gpu"]["replicas_agree"]
+    if exchange == "rotate":
+        assert f["multi_gpu"]["replay"]["bit_equal"]
 
 
 @pytest.mark.timeout(600)
@@ -55,19 +62,21 @@ def test_bench_c4_shape_eight_ranks_rotate():
     user-sharded over 8 ranks -- here 8 gloo ranks sharing cuda:0 with
     per-stratum launches (MF_STRATA_PERSISTENT=0: eight processes share the
     CUs, so a persistent grid cannot count on co-residency; same bits).  The
-    line's own checks must hold at this shape: the eight replicas agree, rank
+    line's own checks must hold at this shape (FP64, the headline's dtype):
+    the eight replicas agree, rank
     0's one-GPU replay of the 8-rank rotation order is bit-equal, and the
     RMSE after 2 epochs is within 1e-3 of the N = 1 schedule's."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus",
-           "8", "--backend", "gloo", "--workload", "c3", "--steps", "1", "--warmup", "1"]
+           "8", "--backend", "gloo", "--workload", "c3", "--steps", "1", "--warmup", "1",
+           "--dtype", "float64"]
     env = dict(os.environ, MF_STRATA_PERSISTENT="0")
     out = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=540, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     lines = [x for x in out.stdout.splitlines() if x.startswith("{")]
     assert len(lines) == 1, out.stdout[-2000:]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 8 and d["config"]["nnz"] == 100_000_000
+    assert d["n_gpus"] == 8 and d["config"]["nnz"] == 100_000_000 and d["dtype"] == "f64"
     assert d["config"]["exchange"] == "rotate"
     m = d["multi_gpu"]
     assert m["replicas_agree"] and len(set(m["replica_fingerprints"])) == 1

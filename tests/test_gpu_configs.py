@@ -54,6 +54,7 @@ def _init(nu, ni, k, dtype, seed=7):
 
 def test_c2_shape_strata_vs_oracle():
     import oracle
+    from matrix_factorization.engine import stratum_order
 
     nu, ni, nnz, k = 100_000, 10_000, 5_000_000, 32
     u, i, r = _synth(nu, ni, nnz)
@@ -68,8 +69,12 @@ def test_c2_shape_strata_vs_oracle():
         P, Q = P0.astype(np.float64), Q0.astype(np.float64)
         bu, bi = np.zeros(nu), np.zeros(ni)
         r64 = eng.r_host.astype(np.float64)
+        # the plan's own draws: at C2 in FP32 (P = 12.8 MB) the XCD-class
+        # stratum order with the L2 hand-off, chosen by prepare_strata
+        if dtype == "float32":
+            assert plan.l2_handoff and plan.order == "xcd" and plan.B % 8 == 0, plan.B
         for ep in range(epochs):
-            seq = rs.permutation(plan.B).astype(np.int32)
+            seq = stratum_order(rs, plan)
             seed = int(rs.randint(0, 2**31 - 1))
             eng.epoch_strata(seq, seed, lr=0.01, reg=0.02)
             eng.sse_async(ep)

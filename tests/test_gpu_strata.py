@@ -203,14 +203,17 @@ def test_deep_pipe_equals_per_stratum_launches(dtype, B, kernel, k, nu, ni, wave
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("kernel,k,waves", [("sigmoid", 32, 8), ("linear", 64, 8), ("rbf", 16, 8),
-                                           ("sigmoid", 32, 4), ("linear", 16, 4)])
-def test_eight_wave_kernels(kernel, k, waves):
-    """The 8-wave strata kernels (plans of half the slots, FP32, k <= 64) and
-    their narrow 4-wave form (the same plan, lane groups half as wide,
-    MF_FLAG_NARROW): the persistent epoch is bit-identical to per-stratum
-    launches, and both are the oracle's sequential sweep in the plan's
-    serial order (FP32 vs FP64: train RMSE within 1e-5)."""
+@pytest.mark.parametrize("kernel,k,waves,dtype", [
+    ("sigmoid", 32, 8, "float32"), ("linear", 64, 8, "float32"), ("rbf", 16, 8, "float32"),
+    ("sigmoid", 32, 4, "float32"), ("linear", 16, 4, "float32"),
+    ("sigmoid", 32, 8, "float64"), ("linear", 20, 8, "float64")])
+def test_eight_wave_kernels(kernel, k, waves, dtype):
+    """The 8-wave strata kernels (plans of half the slots; rows of one vector
+    per lane: FP32 k <= 64, FP64 k <= 32) and their narrow 4-wave form (FP32:
+    the same plan, lane groups half as wide, MF_FLAG_NARROW): the persistent
+    epoch is bit-identical to per-stratum launches, and both are the oracle's
+    sequential sweep in the plan's serial order (FP32 vs FP64: train RMSE
+    within 1e-5; FP64: parameters within 1e-11)."""
     import oracle
 
     nu, ni, nnz = 3000, 800, 120000
@@ -220,7 +223,7 @@ def test_eight_wave_kernels(kernel, k, waves):
     bu = rs.normal(0, 0.1, nu); bi = rs.normal(0, 0.1, ni)
     out = []
     for persistent in (True, False):
-        eng = _engine(u, i, r, nu, ni, k, kernel, "float32", P, Q, bu, bi)
+        eng = _engine(u, i, r, nu, ni, k, kernel, dtype, P, Q, bu, bi)
         plan = eng.prepare_strata(n_blocks=6, waves=waves)
         from matrix_factorization.engine import strata_slots
         assert plan.NS == strata_slots(k, eng.dcode, waves) == strata_slots(k, eng.dcode) // 2
@@ -244,7 +247,10 @@ def test_eight_wave_kernels(kernel, k, waves):
                         bu2, bi2, P2, Q2, lr=0.01, reg=0.02, order=order, **hyp)
     ro = oracle.rmse(eng.u_host, eng.i_host, eng.r_host.astype(np.float64), eng.global_mean,
                      bu2, bi2, P2, Q2, **hyp)
-    assert abs(out[0][4] - ro) < 1e-5
+    assert abs(out[0][4] - ro) < (1e-12 if dtype == "float64" else 1e-5)
+    if dtype == "float64":
+        for g, o in zip(out[0][:4], (P2, Q2, bu2, bi2)):
+            _close(g, o, 1e-11)
 
 
 def test_auto_waves_picks_lower_cost():

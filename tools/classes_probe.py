@@ -34,7 +34,8 @@ def main():
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--dtypes", nargs="+", default=["float32", "float64"])
     ap.add_argument("--classes", type=int, nargs="+", default=[1, 2, 3])
-    ap.add_argument("--blocks", type=int, default=None)
+    ap.add_argument("--blocks", type=int, nargs="*", default=[None],
+                    help="B values to sweep (default: the engine's rule)")
     ap.add_argument("--worlds", type=int, nargs="*", default=[])
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--epochs", type=int, default=8)
@@ -65,11 +66,11 @@ def main():
     n_ep = args.warmup + args.epochs
     for rep in range(args.reps):
         for dt in args.dtypes:
-            for C in args.classes:
+            for C, Bq in [(c, b) for c in args.classes for b in args.blocks]:
                 t0 = time.time()
                 e = SGDEngine(u, i, r, nu, ni, k, kernel, dt, dev, **hyp)
                 e.load_params(P=P0, Q=Q0, bu=np.zeros(nu), bi=np.zeros(ni))
-                pl = e.prepare_strata(n_blocks=args.blocks, classes=C)
+                pl = e.prepare_strata(n_blocks=Bq, classes=C)
                 t_plan = time.time() - t0
                 e._ensure_sse_slots(n_ep)
                 ms = []
@@ -89,6 +90,7 @@ def main():
                 ms = np.asarray(ms)
                 n_ph = len(getattr(pl, "phases", [pl]))
                 run = {"rep": rep, "dtype": dt, "classes": C, "B": pl.B, "phases": n_ph,
+                       "l2_handoff": bool(getattr(pl, "l2_handoff", False)),
                        "NS": pl.NS, "launches_per_epoch": nl,
                        "slot_fill": nnz / pl.n_positions,
                        "steps_per_workgroup": float(np.sum(pl.n_steps) / pl.B),
@@ -105,7 +107,7 @@ def main():
             for W in args.worlds:
                 for C in args.classes:
                     rp = RotationReplay(u, i, r, nu, ni, W, k, kernel, dt, dev,
-                                        n_blocks=args.blocks, classes=C, **hyp)
+                                        n_blocks=args.blocks[0], classes=C, **hyp)
                     rp.load(P0.astype(dt), Q0.astype(dt), np.zeros(nu), np.zeros(ni))
                     per = []
                     for ep in range(n_ep):

@@ -148,11 +148,60 @@ def main():
         del e
         torch.cuda.empty_cache()
 
+    def regrouped(opt, fam):
+        """K groupings: K engines over randomly relabelled users and items
+        (engine 0: the identity), each with its own strata plan; every epoch
+        draws which one runs, and the parameters move to its labelling
+        (device gathers) -- a probe of re-drawing which users and items share
+        a block, before any product support."""
+        K = opt["K"]
+        rk = np.random.RandomState(424242)
+        perms = [(np.arange(nu), np.arange(ni))] + [(rk.permutation(nu), rk.permutation(ni))
+                                                    for _ in range(K - 1)]
+        engines = []
+        for pu, pi in perms:
+            e = SGDEngine(pu[u].astype(np.int32), pi[i].astype(np.int32), r, nu, ni, k, kernel,
+                          args.dtype, dev, **hyp)
+            e.prepare_strata(n_blocks=opt["B"], classes=opt["C"])
+            e.load_params(P=P0, Q=Q0, bu=np.zeros(nu), bi=np.zeros(ni))
+            engines.append(e)
+        dperm = [(torch.from_numpy(pu).to(dev), torch.from_numpy(pi).to(dev)) for pu, pi in perms]
+        out = []
+        for s in args.draw_seeds:
+            e0 = engines[0]
+            e0.load_params(P=P0, Q=Q0, bu=np.zeros(nu), bi=np.zeros(ni))
+            cur, rm = 0, []
+            for ep in range(E):
+                rsd = np.random.RandomState([s, ep])
+                kk = int(rsd.randint(0, K))
+                if kk != cur:      # row of original user x: pu_cur[x] -> pu_kk[x]
+                    a, b = engines[cur], engines[kk]
+                    (pu_a, pi_a), (pu_b, pi_b) = dperm[cur], dperm[kk]
+                    b.P[pu_b] = a.P[pu_a]
+                    b.bu[pu_b] = a.bu[pu_a]
+                    b.Q[pi_b] = a.Q[pi_a]
+                    b.bi[pi_b] = a.bi[pi_a]
+                    cur = kk
+                e = engines[cur]
+                e.epoch_strata(stratum_order(rsd, e.strata), int(rsd.randint(0, 2**31 - 1)),
+                               args.lr, args.reg)
+                e.sse_async(ep)
+                rm.append(e.rmse_values(ep + 1)[ep])
+            out.append({"family": fam, "seed": s, "rmse": rm, "dtype": args.dtype, "K": K,
+                        "B": engines[0].strata.B, "classes": engines[0].strata.classes})
+            log(f"{fam} (K={K}) seed {s}: final {rm[-1]:.7f}")
+        del engines
+        torch.cuda.empty_cache()
+        return out
+
     for var in args.variants:
-        opt = {"C": 1, "B": None}
+        opt = {"C": 1, "B": None, "K": 1}
         for part in var.split("_"):
             opt[part[0]] = int(part[1:])
         fam = "strata" if var == "C1" else f"strata_{var}"
+        if opt["K"] > 1:
+            runs += regrouped(opt, fam)
+            continue
         for s in args.draw_seeds:
             e = fresh()
             pl = e.prepare_strata(n_blocks=opt["B"], classes=opt["C"])

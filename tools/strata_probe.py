@@ -57,7 +57,8 @@ def main():
     for ep in range(2):
         run(stratum_order(rs, plan), ep)
     torch.cuda.synchronize()
-    probe = torch.zeros(4 * B * B, dtype=torch.int64, device="cuda:0")
+    NSQ = plan.n_strata                   # positions per launch (C*B with user-range classes)
+    probe = torch.zeros(4 * NSQ * B, dtype=torch.int64, device="cuda:0")
     _lib.call("mf_strata_set_probe", ctypes.c_void_p(probe.data_ptr()))
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
@@ -67,7 +68,7 @@ def main():
     torch.cuda.synchronize()
     _lib.call("mf_strata_set_probe", None)
     eng.check_strata()
-    st = probe.cpu().numpy().reshape(B, B, 4).astype(np.float64) * 10.0 / 1000.0   # us
+    st = probe.cpu().numpy().reshape(NSQ, B, 4).astype(np.float64) * 10.0 / 1000.0   # us
     if not np.all(st[:, :, 3] > 0):
         print("probe incomplete (per-stratum fallback ran?)")
         return
@@ -77,10 +78,10 @@ def main():
     gap = st[1:, :, 0] - st[:-1, :, 3]
     span = st[:, :, 3].max() - st[:, :, 0].min()
     pl0 = plan.phases[0] if args.rotate else plan
-    steps = np.diff(pl0.bstep).reshape(B, B)             # [s, w]
+    steps = np.diff(pl0.bstep).reshape(NSQ, B)           # [s, w]
     print(f"{args.workload}{' rotate N=%d sub-epoch' % args.rotate if args.rotate else ''}: "
-          f"B={B} NS={plan.NS} epoch kernel {t0.elapsed_time(t1):.3f} ms, "
-          f"stamp span {span / 1e3:.3f} ms, per position {span / B:.2f} us")
+          f"B={B} C={plan.classes} NS={plan.NS} epoch kernel {t0.elapsed_time(t1):.3f} ms, "
+          f"stamp span {span / 1e3:.3f} ms, per position {span / NSQ:.2f} us")
     for name, a in (("wait", wait), ("block", block), ("signal", sig), ("gap", gap)):
         print(f"  {name:6s} mean {a.mean():7.2f} us  p50 {np.median(a):7.2f}  p90 "
               f"{np.percentile(a, 90):7.2f}  max {a.max():7.2f}")
