@@ -249,9 +249,9 @@ int mf_strata_inject_fail(int32_t n_launches);
 /* Rating slots per step of the strata kernel for (n_factors, dtype); -1 on
  * invalid arguments. */
 int32_t mf_strata_slots(int32_t n_factors, int32_t dtype);
-/* The same for a workgroup of `waves` waves: 16 (the default) or, for rows of
- * one vector per lane (FP32 n_factors <= 64, FP64 n_factors <= 32), 8 -- a
- * plan built with that many slots runs the
+/* The same for a workgroup of `waves` waves: 16 (the default) or, FP32 with
+ * n_factors <= 64 or FP64 with n_factors <= 64, 8 -- a plan built with that
+ * many slots runs the
  * 8-wave kernels (blocks whose step count is set by the item degree, not by
  * the slot count); 4 = the narrow form of the 8-wave plan (same slot count,
  * run with MF_FLAG_NARROW; FP32, n_factors a multiple of 4 up to 32); -1

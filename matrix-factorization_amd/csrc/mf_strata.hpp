@@ -837,11 +837,12 @@ inline bool strata_coresident(const void* kfn, int B, size_t lds, int threads) {
 // for plans whose blocks are bound by the item degree rather than by the slot
 // count -- half the slots per step, half the per-step VALU of a CU, about the
 // same number of steps (C2: DESIGN.md section 5).  The 8-wave kernels exist
-// for rows of one vector per lane (FP32 k <= 64, FP64 k <= 32; FP64 since
-// round 4: C2 in FP64 filled 54 % of the 16-wave plan's slots).
+// for rows of one vector per lane (FP32 k <= 64, FP64 k <= 32) and for FP64
+// rows of two (k <= 64) -- FP64 since round 4: C2 in FP64 filled 54 % of the
+// 16-wave plan's slots, C3 with 4 user-range classes 65 %.
 template <typename T, int V>
 constexpr bool strata_has_8_waves() {
-    return V == 1;
+    return V == 1 || (std::is_same<T, double>::value && V == 2);
 }
 
 // the narrow form (MF_FLAG_NARROW): 4 waves whose lane groups are half as

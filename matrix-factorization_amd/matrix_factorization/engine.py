@@ -622,17 +622,19 @@ class SGDEngine:
         self.colored = offs
         return len(offs) - 1
 
-    # user-range classes of the strata plans (StrataPlan.classes): None = 1;
-    # env MF_STRATA_CLASSES overrides
-    strata_classes: Optional[int] = None
+    # user-range classes of the strata plans (StrataPlan.classes): "auto" /
+    # None = by the plan (auto_classes), or 1..4; env MF_STRATA_CLASSES
+    # overrides
+    strata_classes = "auto"
 
-    def _classes(self, classes: Optional[int]) -> int:
+    def _classes(self, classes) -> Optional[int]:
+        """The classes asked for, or None for the automatic choice."""
         if classes is None and os.environ.get("MF_STRATA_CLASSES"):
-            classes = int(os.environ["MF_STRATA_CLASSES"])
+            classes = os.environ["MF_STRATA_CLASSES"]
         if classes is None:
             classes = self.strata_classes
-        if classes is None:
-            classes = 1
+        if classes is None or classes == "auto":
+            return None
         classes = int(classes)
         if not 1 <= classes <= _lib.MF_STRATA_MAX_CLASSES:
             raise ValueError(f"strata classes must be in [1, {_lib.MF_STRATA_MAX_CLASSES}], "
@@ -666,11 +668,16 @@ class SGDEngine:
 
         ``classes``: user-range classes C (C*B user ranges, C*B strata per
         epoch; the persistent kernel then hands a user range over with C - 1
-        blocks of slack).  None = ``strata_classes`` / env
-        MF_STRATA_CLASSES, else 1."""
+        blocks of slack, and an item meets 1/C of a block's ratings per user
+        range).  None = ``strata_classes`` / env MF_STRATA_CLASSES; "auto"
+        (the default) = ``auto_classes`` for the engine's own B (n_blocks
+        None, no item_bounds), else 1."""
         if self.colored is not None or self.strata is not None:
             raise RuntimeError("ratings already permuted by another schedule")
         classes = self._classes(classes)
+        auto_classes = classes is None
+        if auto_classes:
+            classes = 1
         env = os.environ.get("MF_STRATA_WAVES")
         if waves is None and env in ("4", "8", "16"):
             waves = int(env)
@@ -688,6 +695,10 @@ class SGDEngine:
         auto_l2 = False
         if phases is None and n_blocks is None:
             phases, n_blocks, bounds = self._item_phases(classes)
+            if auto_classes:
+                classes = self.auto_classes(n_blocks)
+                if classes > 1:
+                    phases, n_blocks, bounds = self._item_phases(classes)
             if phases == 1 and classes == 1 and self._l2_handoff_fits():
                 B8 = min(self._cus(), -(-n_blocks // XCD_CLASSES) * XCD_CLASSES)
                 b8 = self._bounds_for(B8) if B8 >= 2 * XCD_CLASSES else None
@@ -703,6 +714,26 @@ class SGDEngine:
                 plan.l2_handoff, plan.order = True, "xcd"
         self.strata = plan
         return plan
+
+    # the automatic choice of user-range classes: the
+    # strata order trains measurably slower than the reference's random order
+    # when an item meets many ratings of one user range inside a block -- at
+    # C3 (linear, rank 64, 3.9 ratings per item and block) train RMSE after 20
+    # epochs +4.7e-5 over the reference's mean (12 shuffle seeds, SD 8e-6),
+    # +2.0e-5 with 2 classes, +1.1e-5 with 4 (profiles/r04/seed_spread_*);
+    # the sigmoid kernel at C2 (7.2 per block, effective step scaled by the
+    # sigmoid's derivative) shows none (+1.1e-6, profiles/r04/order_bias_cpu_c2.json)
+    AUTO_CLASSES = 4
+    AUTO_CLASSES_MIN_DEGREE = 2.0
+
+    def auto_classes(self, B: int) -> int:
+        """Classes for the engine's own plan of B workgroups: AUTO_CLASSES for
+        the linear kernel when an item meets at least AUTO_CLASSES_MIN_DEGREE
+        ratings per user range of the one-class plan, else 1."""
+        if self.kernel != "linear" or self.n == 0 or B < 1:
+            return 1
+        deg = self.n / float(max(self.n_items, 1) * B)
+        return self.AUTO_CLASSES if deg >= self.AUTO_CLASSES_MIN_DEGREE else 1
 
     def _l2_handoff_fits(self) -> bool:
         """MF_FLAG_L2_HANDOFF by the plan (env MF_STRATA_L2=0 / 1 forces it

@@ -22,6 +22,11 @@ Three keyword arguments are new and default to the reference's behaviour:
               RCCL all-reduce of the item-row deltas once per epoch,
               distributed.fit_sharded) and every rank ends with the full
               model.  Needs schedule "strata" or "colored".
+``strata_classes``  schedule "strata" only: user-range classes of the plan,
+              "auto" (default: 4 for the linear kernel where an item meets
+              >= 2 ratings per user range and block, else 1 -- the order
+              then trains like the reference's random order, DESIGN.md
+              section 3) or 1..4 (1: the fastest plan).
 ``exchange``  process-group mode only: "rotate" (default; exact -- items are
               cut into one range per rank and the ranges are passed round the
               ring between sub-epochs, so every rating is applied with the
@@ -95,13 +100,15 @@ class KernelMF(RecommenderBase):
                  init_sd: float = 0.1, min_rating: int = 0, max_rating: int = 5,
                  verbose: int = 1, dtype: str = "float64",
                  schedule: str = "exact", device=None, distributed: bool = False,
-                 exchange: str = "rotate"):
+                 exchange: str = "rotate", strata_classes="auto"):
         if kernel not in ("linear", "sigmoid", "rbf"):
             raise ValueError("Kernel must be one of linear, sigmoid, or rbf")
         if schedule not in ("exact", "colored", "strata"):
             raise ValueError("schedule must be 'exact', 'colored' or 'strata'")
         if exchange not in EXCHANGES:
             raise ValueError(f"exchange must be one of {EXCHANGES}")
+        if strata_classes != "auto" and strata_classes not in (1, 2, 3, 4):
+            raise ValueError("strata_classes must be 'auto' or 1..4")
         canonical_dtype(dtype)
         super().__init__(min_rating=min_rating, max_rating=max_rating, verbose=verbose)
         self.n_factors = n_factors
@@ -118,6 +125,7 @@ class KernelMF(RecommenderBase):
         self.device = device
         self.distributed = distributed
         self.exchange = exchange
+        self.strata_classes = strata_classes
 
     # ----------------------------------------------------- device state
     def _make_engine(self, X: pd.DataFrame, n_users: int, n_items: int,
@@ -133,6 +141,7 @@ class KernelMF(RecommenderBase):
                         self.n_factors, self.kernel, self.dtype, self.device,
                         gamma=self.gamma, min_rating=self.min_rating,
                         max_rating=self.max_rating, global_mean=self.global_mean)
+        eng.strata_classes = getattr(self, "strata_classes", "auto")
         if schedule == "strata" and n:
             eng.prepare_strata()
         elif schedule == "colored" and n:
@@ -198,7 +207,8 @@ class KernelMF(RecommenderBase):
         # build-only arguments added after a pickle was written take their
         # defaults (the reference's pickles have none of them)
         for key, default in (("dtype", "float64"), ("schedule", "exact"), ("device", None),
-                             ("distributed", False), ("exchange", "rotate")):
+                             ("distributed", False), ("exchange", "rotate"),
+                             ("strata_classes", "auto")):
             state.setdefault(key, default)
         self.__dict__.update(state)
         _warn_if_no_device()

@@ -97,21 +97,25 @@ def test_c2_shape_strata_vs_oracle():
 def test_c3_shape_persistent_equals_per_stratum(c3_data):
     import torch
 
+    from matrix_factorization.engine import stratum_order
+
     u, i, r = c3_data
     nu, ni, k = 1_000_000, 100_000, 64
     P0, Q0 = _init(nu, ni, k, np.float32)
     eng = _engine(u, i, r, nu, ni, k, "linear", "float32")
     plan = eng.prepare_strata()
-    assert plan.B == 256
+    # the engine's own plan at C3: B = 256 and, linear kernel with 3.9
+    # ratings per item and block, 4 user-range classes
+    assert plan.B == 256 and plan.classes == 4 and plan.n_strata == 1024
     rs = np.random.RandomState(5)
-    seqs = [rs.permutation(plan.B).astype(np.int32) for _ in range(2)]
+    seqs = [stratum_order(rs, plan) for _ in range(2)]
     seeds = [int(x) for x in rs.randint(0, 2**31 - 1, 2)]
     out = []
     for persistent in (False, True):
         eng.load_params(P0, Q0, np.zeros(nu), np.zeros(ni))
         _, n_launch = eng.epoch_strata(seqs[0], seeds[0], 0.01, 0.02, timing=True,
                                        persistent=persistent)
-        assert n_launch == (1 if persistent else plan.B)
+        assert n_launch == (1 if persistent else plan.n_strata)
         eng.check_strata()
         out.append([t.clone() for t in (eng.P, eng.Q, eng.bu, eng.bi)])
     for a, b in zip(*out):

@@ -347,7 +347,7 @@ def test_item_phases_chosen_when_slabs_exceed_lds():
     over one workgroup per CU (FP64 rank 128 over 60K items: 62 MB of rows,
     236 KiB per workgroup at B = 256 > 160 KiB of LDS), and the phased
     persistent epoch equals its per-stratum launches."""
-    from matrix_factorization.engine import PhasedStrata
+    from matrix_factorization.engine import PhasedStrata, stratum_order
 
     nu, ni, nnz, k = 4000, 60000, 200000, 128
     u, i, r = _synthetic(41, nu, ni, nnz)
@@ -357,7 +357,7 @@ def test_item_phases_chosen_when_slabs_exceed_lds():
     plan = eng.prepare_strata()
     assert isinstance(plan, PhasedStrata), "60K items of FP64 rank 128 (62 MB) need phases"
     assert plan.B <= eng._cus()
-    seq = rs.permutation(plan.B).astype(np.int32)
+    seq = stratum_order(rs, plan)
     ms = eng.epoch_strata(seq, 5, lr=0.01, reg=0.02, timing=True)
     assert ms[1] == len(plan.phases)                # persistent: one launch per phase
     eng.check_strata()

@@ -324,6 +324,29 @@ def test_constructor_validation_and_sklearn_clone():
     c = clone(m)
     assert c.get_params() == m.get_params()
     assert c.dtype == "float32" and c.schedule == "colored"
+    assert m.strata_classes == "auto" and clone(KernelMF(strata_classes=2)).strata_classes == 2
+    with pytest.raises(ValueError, match="strata_classes"):
+        KernelMF(strata_classes=5)
+
+
+def test_auto_classes_rule():
+    """SGDEngine.auto_classes: 4 user-range classes for the linear kernel
+    where an item meets >= 2 ratings per user range of the one-class plan
+    (C3: 100M / (100K items x B 256) = 3.9), else 1 (sigmoid / rbf, sparse
+    blocks, the bias model)."""
+    from types import SimpleNamespace
+
+    from matrix_factorization.engine import SGDEngine
+
+    def eng(kernel, n, n_items):
+        return SimpleNamespace(kernel=kernel, n=n, n_items=n_items,
+                               AUTO_CLASSES=SGDEngine.AUTO_CLASSES,
+                               AUTO_CLASSES_MIN_DEGREE=SGDEngine.AUTO_CLASSES_MIN_DEGREE)
+
+    assert SGDEngine.auto_classes(eng("linear", 100_000_000, 100_000), 256) == 4
+    assert SGDEngine.auto_classes(eng("sigmoid", 5_000_000, 10_000), 69) == 1
+    assert SGDEngine.auto_classes(eng("linear", 1_000_000, 100_000), 256) == 1
+    assert SGDEngine.auto_classes(eng("bias", 100_000_000, 100_000), 256) == 1
 
 
 def test_product_has_no_cpu_path(monkeypatch):

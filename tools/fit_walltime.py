@@ -63,6 +63,24 @@ def main():
         return wrap
 
     KernelMF._preprocess_data = timed("preprocess", KernelMF._preprocess_data)
+    # the native preprocessing calls (some run on worker threads: wall time of
+    # each call, summed per function)
+    from matrix_factorization import _prep
+    import matrix_factorization.recommender_base as rbm
+    calls = {}
+
+    def timed_call(name, fn):
+        def wrap(*a, **kw):
+            t = time.perf_counter()
+            out = fn(*a, **kw)
+            calls[name] = calls.get(name, 0.0) + time.perf_counter() - t
+            return out
+        return wrap
+
+    for name in ("legacy_permutation", "pairs_duplicated", "factorize", "gather"):
+        setattr(_prep, name, timed_call(name, getattr(_prep, name)))
+    rbm.RecommenderBase._fit_maps_native = timed_call(
+        "fit_maps_native", rbm.RecommenderBase._fit_maps_native)
     # since round 4 the engine (upload, evaluation order, strata plan) is built
     # on a worker thread while fit() draws the initial factors
     KernelMF._make_engine = timed("engine_build_worker", KernelMF._make_engine)
@@ -131,6 +149,7 @@ def main():
                                       "normal draws; init_beside_engine_build is the wall time "
                                       "of both together"),
                       "phases_s": {k: round(v, 3) for k, v in phases.items()},
+                      "prep_calls_s": {k: round(v, 3) for k, v in calls.items()},
                       "epoch_ms_events": ep_ms,
                       "epoch_ms_events_note": ("hipEvents between consecutive epochs of "
                                                "fit_epochs (SGD sweep + RMSE pass each); "

@@ -47,11 +47,11 @@ def log(msg):
     print(f"[order_bias {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def setup(nu, ni, nnz, k):
+def setup(nu, ni, nnz, k, kernel="linear"):
     import bench
     u, i, r = bench.synth(nu, ni, nnz)
     rs = np.random.RandomState(7)
-    G.update(u=u, i=i, r=r.astype(np.float64), nu=nu, ni=ni, k=k,
+    G.update(u=u, i=i, r=r.astype(np.float64), nu=nu, ni=ni, k=k, kernel=kernel,
              P0=rs.normal(0, 0.1, (nu, k)), Q0=rs.normal(0, 0.1, (ni, k)),
              mu=float(np.mean(r, dtype=np.float64)))
 
@@ -96,7 +96,7 @@ def run(job):
     P, Q = G["P0"].copy(), G["Q0"].copy()
     bu, bi = np.zeros(nu), np.zeros(ni)
     mu = G["mu"]
-    B, C, K = 256, 1, 0
+    B, C, K = G.get("B", 256), 1, 0
     for part in arm.split("_")[1:]:
         if part[0] == "B":
             B = int(part[1:])
@@ -134,9 +134,10 @@ def run(job):
         else:
             rsd = np.random.RandomState([seed, ep])
             o = plan.serial_order(stratum_order(rsd, plan), int(rsd.randint(0, 2**31 - 1)))
-        oracle.sgd_pass(u, i, r, mu, bu, bi, P, Q, lr=lr, reg=reg, order=o)
+        hyp = dict(kernel=G["kernel"], gamma=1.0 / G["k"], min_rating=1.0, max_rating=5.0)
+        oracle.sgd_pass(u, i, r, mu, bu, bi, P, Q, lr=lr, reg=reg, order=o, **hyp)
         if ep + 1 in record:
-            out[ep + 1] = oracle.rmse(u, i, r, mu, bu, bi, P, Q)
+            out[ep + 1] = oracle.rmse(u, i, r, mu, bu, bi, P, Q, **hyp)
     return {"arm": arm, "seed": seed, "rmse": out, "s": time.time() - t0}
 
 
@@ -151,6 +152,8 @@ def main():
     ap.add_argument("--items", type=int, default=10_000)
     ap.add_argument("--nnz", type=int, default=10_000_000)
     ap.add_argument("--k", type=int, default=64)
+    ap.add_argument("--kernel", default="linear")
+    ap.add_argument("--blocks", type=int, default=256, help="B of the strata arms")
     ap.add_argument("--workers", type=int, default=8)
     ap.add_argument("--out", default=None)
     ap.add_argument("--merge", nargs="*", default=None,
@@ -165,7 +168,8 @@ def main():
         for x in runs:
             x["rmse"] = {int(k): v for k, v in x["rmse"].items()}
         return summarize(args, runs)
-    setup(args.users, args.items, args.nnz, args.k)
+    setup(args.users, args.items, args.nnz, args.k, args.kernel)
+    G["B"] = args.blocks
     import oracle
     oracle.lib()                                   # build / load before forking
     jobs = [(a, s, args.epochs, set(args.record), 0.01, 0.02)
