@@ -571,6 +571,9 @@ void mf_strata_plan_free(mf_strata_plan* plan);
  *     RandomState.choice(n, n, replace=False)); on the row order it is the
  *     per-epoch np.random.shuffle (kernel_matrix_factorization.py:371).
  *     n <= 2^32 + 1 (NumPy's 32-bit draw branch); MF_ERR_INVALID otherwise.
+ * mf_legacy_permutation  out = np.random.permutation(n) (int64), the same
+ *     draws as mf_legacy_shuffle of arange(n), swapped on 4-byte elements
+ *     while n < 2^31.
  * mf_pairs_duplicated    *has_dup = 1 iff two rows hold the same (a, b)
  *     pair of integer ids (X.duplicated(subset=[user_id, item_id]).sum()
  *     != 0, :127-128).
@@ -578,13 +581,24 @@ void mf_strata_plan_free(mf_strata_plan* plan);
  *     X[col].unique() + the id map of the shuffled frame (:135-140):
  *     uniques[0..*n_uniques) in first-appearance order (capacity n) and
  *     codes[p] = position of vals[p] in uniques.
+ * mf_id_range            *lo / *hi = min / max of vals (n > 0).
+ * mf_first_appearance    pd.factorize(vals[perm], sort=False) given dense ids
+ *     of the unshuffled column: dense[p] - base in [0, n_dense) (the ids
+ *     themselves when they span a small range, else mf_factorize's codes of
+ *     the unshuffled column), n_dense <= 2^32 - 1.  codes[t] = code of row
+ *     perm[t]; order[0..*n_uniques) = the dense ids in code order (capacity
+ *     n_dense), so uniques = base + order or the unshuffled uniques[order].
  * mf_gather              dst[p] = src[idx[p]], idx[p] in [0, n_src), for
  *     elem_bytes 4 or 8.
  * Threads: min(16, cores) unless MF_HOST_THREADS is set. */
 int mf_legacy_shuffle(uint32_t* mt_key, int32_t* mt_pos, int64_t* data, int64_t n);
+int mf_legacy_permutation(uint32_t* mt_key, int32_t* mt_pos, int64_t* out, int64_t n);
 int mf_pairs_duplicated(const int64_t* a, const int64_t* b, int64_t n, int32_t* has_dup);
 int mf_factorize(const int64_t* vals, int64_t n, int64_t* codes, int64_t* uniques,
                  int64_t* n_uniques);
+int mf_id_range(const int64_t* vals, int64_t n, int64_t* lo, int64_t* hi);
+int mf_first_appearance(const int64_t* dense, int64_t base, int64_t n_dense, const int64_t* perm,
+                        int64_t n, int64_t* codes, int64_t* order, int64_t* n_uniques);
 int mf_gather(const void* src, int64_t n_src, int32_t elem_bytes, const int64_t* idx, int64_t n,
               void* dst);
 /* 64-bit fingerprint of a HOST buffer (threaded, not cryptographic): lets the

@@ -21,8 +21,13 @@
 //                        per-bucket hash table sees each value's first row
 //                        first; code = number of first rows before it
 //                        (bitmap + prefix popcount).
+//   mf_first_appearance  pd.factorize of the shuffled column from dense ids
+//                        of the unshuffled one (computed while the
+//                        permutation is drawn): first shuffled position per
+//                        id by atomic min, ranks by bitmap + prefix popcount.
 //   mf_gather            threaded, prefetched dst[p] = src[idx[p]].
 #include <algorithm>
+#include <climits>
 #include <atomic>
 #include <cstdint>
 #include <cstdlib>
@@ -102,25 +107,13 @@ struct MT {
 
 }  // namespace
 
-extern "C" int mf_legacy_shuffle(uint32_t* mt_key, int32_t* mt_pos, int64_t* data, int64_t n) {
-    if (!mt_key || !mt_pos || (n > 0 && !data) || n < 0) {
-        set_error("mf_legacy_shuffle: null pointer or negative n");
-        return MF_ERR_INVALID;
-    }
-    if (n - 1 > (int64_t)0xffffffffLL) {
-        set_error("mf_legacy_shuffle: n = %lld exceeds the 32-bit draw range", (long long)n);
-        return MF_ERR_INVALID;
-    }
-    if (*mt_pos < 0 || *mt_pos > kN) {
-        set_error("mf_legacy_shuffle: MT19937 position %d outside [0, %d]", *mt_pos, kN);
-        return MF_ERR_INVALID;
-    }
-    MT mt;
-    std::memcpy(mt.key, mt_key, sizeof(mt.key));
-    mt.pos = *mt_pos;
-    // Swap targets are drawn kWin positions ahead of the swap that uses them
-    // (the draws do not depend on the data) so the random line is in cache
-    // when the swap reaches it.
+namespace {
+
+// NumPy's _shuffle_raw on x[0..n): swap targets drawn kWin positions ahead of
+// the swap that uses them (the draws do not depend on the data) so the
+// random line is in cache when the swap reaches it.
+template <typename E>
+void shuffle_raw(MT& mt, E* data, int64_t n) {
     constexpr int kWin = 64;
     uint32_t ring[kWin];
     int64_t i = n - 1, drawn = n - 1;  // next swap index / next index to draw for
@@ -138,9 +131,73 @@ extern "C" int mf_legacy_shuffle(uint32_t* mt_key, int32_t* mt_pos, int64_t* dat
             __builtin_prefetch(data + jn, 1, 1);
             --drawn;
         }
-        const int64_t t = data[i];
+        const E t = data[i];
         data[i] = data[j];
         data[j] = t;
+    }
+}
+
+int load_mt(MT& mt, const uint32_t* mt_key, const int32_t* mt_pos, int64_t n, const char* who) {
+    if (n - 1 > (int64_t)0xffffffffLL) {
+        set_error("%s: n = %lld exceeds the 32-bit draw range", who, (long long)n);
+        return MF_ERR_INVALID;
+    }
+    if (*mt_pos < 0 || *mt_pos > kN) {
+        set_error("%s: MT19937 position %d outside [0, %d]", who, *mt_pos, kN);
+        return MF_ERR_INVALID;
+    }
+    std::memcpy(mt.key, mt_key, sizeof(mt.key));
+    mt.pos = *mt_pos;
+    return MF_OK;
+}
+
+}  // namespace
+
+extern "C" int mf_legacy_shuffle(uint32_t* mt_key, int32_t* mt_pos, int64_t* data, int64_t n) {
+    if (!mt_key || !mt_pos || (n > 0 && !data) || n < 0) {
+        set_error("mf_legacy_shuffle: null pointer or negative n");
+        return MF_ERR_INVALID;
+    }
+    MT mt;
+    if (const int rc = load_mt(mt, mt_key, mt_pos, n, "mf_legacy_shuffle")) return rc;
+    shuffle_raw(mt, data, n);
+    std::memcpy(mt_key, mt.key, sizeof(mt.key));
+    *mt_pos = mt.pos;
+    return MF_OK;
+}
+
+// np.random.permutation(n): the shuffle of arange(n) run on 4-byte elements
+// while n < 2^31 (the same draws and swaps on half the bytes), widened into
+// out afterwards.
+extern "C" int mf_legacy_permutation(uint32_t* mt_key, int32_t* mt_pos, int64_t* out, int64_t n) {
+    if (!mt_key || !mt_pos || (n > 0 && !out) || n < 0) {
+        set_error("mf_legacy_permutation: null pointer or negative n");
+        return MF_ERR_INVALID;
+    }
+    MT mt;
+    if (const int rc = load_mt(mt, mt_key, mt_pos, n, "mf_legacy_permutation")) return rc;
+    const int T = host_threads();
+    if (n >= ((int64_t)1 << 31)) {
+        parallel_chunks(n, T, [&](int, int64_t a, int64_t b) {
+            for (int64_t p = a; p < b; ++p) out[p] = p;
+        });
+        shuffle_raw(mt, out, n);
+    } else {
+        big_ptr<uint32_t> tmp{nullptr, MapFree{0}};
+        try {
+            tmp = big_alloc<uint32_t>(n);
+            if (!tmp) throw std::bad_alloc();
+        } catch (const std::bad_alloc&) {
+            set_error("mf_legacy_permutation: cannot allocate %lld rows", (long long)n);
+            return MF_ERR_NOMEM;
+        }
+        parallel_chunks(n, T, [&](int, int64_t a, int64_t b) {
+            for (int64_t p = a; p < b; ++p) tmp[p] = (uint32_t)p;
+        });
+        shuffle_raw(mt, tmp.get(), n);
+        parallel_chunks(n, T, [&](int, int64_t a, int64_t b) {
+            for (int64_t p = a; p < b; ++p) out[p] = tmp[p];
+        });
     }
     std::memcpy(mt_key, mt.key, sizeof(mt.key));
     *mt_pos = mt.pos;
@@ -292,6 +349,122 @@ extern "C" int mf_factorize(const int64_t* vals, int64_t n, int64_t* codes, int6
         for (int64_t q = 0; q < m; ++q) codes[s[q]] = f[(size_t)l[q]];
     });
     *n_uniques = U;
+    return MF_OK;
+}
+
+extern "C" int mf_id_range(const int64_t* vals, int64_t n, int64_t* lo, int64_t* hi) {
+    if (n < 0 || !lo || !hi || (n > 0 && !vals)) {
+        set_error("mf_id_range: bad arguments");
+        return MF_ERR_INVALID;
+    }
+    const int T = host_threads();
+    std::vector<int64_t> mn((size_t)T, INT64_MAX), mx((size_t)T, INT64_MIN);
+    parallel_chunks(n, T, [&](int t, int64_t a, int64_t b) {
+        int64_t l = INT64_MAX, h = INT64_MIN;
+        for (int64_t p = a; p < b; ++p) {
+            l = std::min(l, vals[p]);
+            h = std::max(h, vals[p]);
+        }
+        mn[(size_t)t] = l;
+        mx[(size_t)t] = h;
+    });
+    *lo = *std::min_element(mn.begin(), mn.end());
+    *hi = *std::max_element(mx.begin(), mx.end());
+    return MF_OK;
+}
+
+// pd.factorize(vals[perm], sort=False) from dense ids of the UNSHUFFLED
+// column (dense[p] - base in [0, n_dense): the id itself when the ids span a
+// small range, else mf_factorize's codes of the unshuffled column -- either
+// is ready before the permutation is drawn).  The code of a dense id is the
+// rank of its first position t in the shuffled order: per id the minimum t
+// (an atomic min over threads that each walk a chunk of t), a bitmap of
+// those first positions, and its prefix popcounts.
+extern "C" int mf_first_appearance(const int64_t* dense, int64_t base, int64_t n_dense,
+                                   const int64_t* perm, int64_t n, int64_t* codes,
+                                   int64_t* order, int64_t* n_uniques) {
+    if (n < 0 || n_dense < 0 || n_dense > (int64_t)UINT32_MAX || !n_uniques ||
+        (n > 0 && (!dense || !perm || !codes || !order || n_dense == 0))) {
+        set_error("mf_first_appearance: bad arguments");
+        return MF_ERR_INVALID;
+    }
+    *n_uniques = 0;
+    if (n == 0) return MF_OK;
+    const int T = host_threads();
+    const int64_t nw = (n + 63) >> 6;
+    big_ptr<int64_t> first{nullptr, MapFree{0}};
+    big_ptr<uint32_t> g{nullptr, MapFree{0}};
+    big_ptr<uint64_t> bits{nullptr, MapFree{0}};
+    try {
+        first = big_alloc<int64_t>(n_dense);
+        g = big_alloc<uint32_t>(n);
+        bits = big_alloc<uint64_t>(nw);
+        if (!first || !g || !bits) throw std::bad_alloc();
+    } catch (const std::bad_alloc&) {
+        set_error("mf_first_appearance: cannot allocate %lld rows", (long long)n);
+        return MF_ERR_NOMEM;
+    }
+    parallel_chunks(n_dense, T, [&](int, int64_t a, int64_t b) {
+        for (int64_t d = a; d < b; ++d) first[d] = n;
+    });
+    parallel_chunks(nw, T, [&](int, int64_t a, int64_t b) {
+        for (int64_t w = a; w < b; ++w) bits[w] = 0;
+    });
+    std::atomic<int> bad{0};
+    // 1. dense id of every shuffled row; its first shuffled position
+    parallel_chunks(n, T, [&](int, int64_t a, int64_t b) {
+        constexpr int kAhead = 16;
+        for (int64_t t = a; t < b; ++t) {
+            if (t + kAhead < b) {
+                const int64_t q = perm[t + kAhead];
+                if (q >= 0 && q < n) __builtin_prefetch(dense + q, 0, 0);
+            }
+            const int64_t p = perm[t];
+            if (p < 0 || p >= n) {
+                bad.store(1);
+                return;
+            }
+            const int64_t d = dense[p] - base;
+            if (d < 0 || d >= n_dense) {
+                bad.store(1);
+                return;
+            }
+            g[t] = (uint32_t)d;
+            int64_t cur = __atomic_load_n(&first[d], __ATOMIC_RELAXED);
+            while (t < cur && !__atomic_compare_exchange_n(&first[d], &cur, t, true,
+                                                           __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+            }
+        }
+    });
+    if (bad.load()) {
+        set_error("mf_first_appearance: permutation or dense id out of range");
+        return MF_ERR_INVALID;
+    }
+    // 2. bitmap of first positions, prefix popcounts
+    parallel_chunks(n_dense, T, [&](int, int64_t a, int64_t b) {
+        for (int64_t d = a; d < b; ++d) {
+            const int64_t f = first[d];
+            if (f < n) __atomic_fetch_or(&bits[f >> 6], 1ull << (f & 63), __ATOMIC_RELAXED);
+        }
+    });
+    std::vector<int64_t> wpre((size_t)nw + 1);
+    wpre[0] = 0;
+    for (int64_t w = 0; w < nw; ++w) wpre[w + 1] = wpre[w] + __builtin_popcountll(bits[w]);
+    // 3. code of every dense id (in place of its first position), ids in code order
+    parallel_chunks(n_dense, T, [&](int, int64_t a, int64_t b) {
+        for (int64_t d = a; d < b; ++d) {
+            const int64_t f = first[d];
+            if (f >= n) continue;
+            const int64_t c = wpre[f >> 6] + __builtin_popcountll(bits[f >> 6] & ((1ull << (f & 63)) - 1));
+            first[d] = c;
+            order[c] = d;
+        }
+    });
+    // 4. codes of the shuffled rows
+    parallel_chunks(n, T, [&](int, int64_t a, int64_t b) {
+        for (int64_t t = a; t < b; ++t) codes[t] = first[g[t]];
+    });
+    *n_uniques = wpre[nw];
     return MF_OK;
 }
 

@@ -120,8 +120,11 @@ SIGNATURES = {
     "mf_strata_set_probe": (ctypes.c_int, [_P]),
     "mf_strata_inject_fail": (ctypes.c_int, [_I32]),
     "mf_legacy_shuffle": (ctypes.c_int, [_P, _P, _P, _I64]),
+    "mf_legacy_permutation": (ctypes.c_int, [_P, _P, _P, _I64]),
     "mf_pairs_duplicated": (ctypes.c_int, [_P, _P, _I64, _P]),
     "mf_factorize": (ctypes.c_int, [_P, _I64, _P, _P, _P]),
+    "mf_id_range": (ctypes.c_int, [_P, _I64, _P, _P]),
+    "mf_first_appearance": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _P, _P]),
     "mf_gather": (ctypes.c_int, [_P, _I64, _I32, _P, _I64, _P]),
     "mf_fingerprint": (ctypes.c_uint64, [_P, _I64]),
 }

@@ -44,8 +44,14 @@ def legacy_shuffle_(a: np.ndarray) -> None:
 
 def legacy_permutation(n: int) -> np.ndarray:
     """``np.random.permutation(n)`` (int64), same draws."""
-    perm = np.arange(n, dtype=np.int64)
-    legacy_shuffle_(perm)
+    st = np.random.get_state()
+    if n > _MAX_N or st[0] != "MT19937":        # pragma: no cover - NumPy's own path
+        return np.random.permutation(n).astype(np.int64)
+    perm = np.empty(n, np.int64)
+    key = np.ascontiguousarray(st[1], dtype=np.uint32).copy()
+    pos = ctypes.c_int32(int(st[2]))
+    _lib.call("mf_legacy_permutation", _ptr(key), ctypes.addressof(pos), _ptr(perm), n)
+    np.random.set_state(("MT19937", key, pos.value, st[3], st[4]))
     return perm
 
 
@@ -81,6 +87,46 @@ def factorize(vals: np.ndarray):
     _lib.call("mf_factorize", _ptr(vals), len(vals), _ptr(codes), _ptr(uniques),
               ctypes.addressof(nu))
     return codes, uniques[: nu.value].copy()
+
+
+# ids spanning at most n + this many values are their own dense ids
+DIRECT_SPAN_SLACK = 1 << 20
+
+
+def dense_ids(vals: np.ndarray):
+    """Dense ids of an UNSHUFFLED int64 column for ``factorize_shuffled``:
+    (dense, base, n_dense, uniques) -- the column itself and its minimum when
+    its values span at most len + DIRECT_SPAN_SLACK integers, else
+    ``factorize``'s codes and uniques.  Needs no permutation, so fit() runs it
+    while the permutation is drawn."""
+    vals = np.ascontiguousarray(vals, dtype=np.int64)
+    if len(vals) == 0:
+        return vals, 0, 0, np.empty(0, np.int64)
+    lo, hi = ctypes.c_int64(0), ctypes.c_int64(0)
+    _lib.call("mf_id_range", _ptr(vals), len(vals), ctypes.addressof(lo), ctypes.addressof(hi))
+    span = int(hi.value) - int(lo.value) + 1
+    if span <= min(len(vals) + DIRECT_SPAN_SLACK, (1 << 32) - 1):
+        return vals, int(lo.value), span, None
+    codes, uniq = factorize(vals)
+    return codes, 0, len(uniq), uniq
+
+
+def factorize_shuffled(dense, perm: np.ndarray):
+    """``pd.factorize(vals[perm], sort=False)`` from ``dense_ids(vals)``:
+    (codes int64, uniques int64 in first-appearance order of the shuffled
+    column)."""
+    d, base, nd, uniq = dense
+    perm = np.ascontiguousarray(perm, dtype=np.int64)
+    if len(perm) != len(d):
+        raise ValueError("permutation and column differ in length")
+    codes = np.empty(len(perm), np.int64)
+    order = np.empty(max(nd, 1), np.int64)
+    nu = ctypes.c_int64(0)
+    if len(perm):
+        _lib.call("mf_first_appearance", _ptr(d), base, nd, _ptr(perm), len(perm),
+                  _ptr(codes), _ptr(order), ctypes.addressof(nu))
+    order = order[: nu.value]
+    return codes, (order + base if uniq is None else uniq[order])
 
 
 def gather(src: np.ndarray, idx: np.ndarray) -> np.ndarray:

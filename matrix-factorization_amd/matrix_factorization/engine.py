@@ -421,6 +421,21 @@ def _contiguous_empty(shape, dtype, dev) -> Optional[torch.Tensor]:
     return t
 
 
+AUTO_CLASSES = 4
+AUTO_CLASSES_MIN_DEGREE = 2.0
+
+
+def auto_strata_classes(kernel: str, n: int, n_items: int, B: int) -> int:
+    """The automatic user-range classes of a plan of B workgroups over n
+    ratings (SGDEngine.auto_classes): AUTO_CLASSES for
+    the linear kernel when an item meets at least AUTO_CLASSES_MIN_DEGREE
+    ratings per user range of the one-class plan, else 1."""
+    if kernel != "linear" or n == 0 or B < 1:
+        return 1
+    deg = n / float(max(n_items, 1) * B)
+    return AUTO_CLASSES if deg >= AUTO_CLASSES_MIN_DEGREE else 1
+
+
 def stratum_order(rs, nb, mode: Optional[str] = None, classes: Optional[int] = None) -> np.ndarray:
     """The stratum order of one epoch, drawn from ``rs`` (a RandomState or
     the ``np.random`` module).  ``nb``: B, or a strata plan (its B and its
@@ -723,17 +738,14 @@ class SGDEngine:
     # +2.0e-5 with 2 classes, +1.1e-5 with 4 (profiles/r04/seed_spread_*);
     # the sigmoid kernel at C2 (7.2 per block, effective step scaled by the
     # sigmoid's derivative) shows none (+1.1e-6, profiles/r04/order_bias_cpu_c2.json)
-    AUTO_CLASSES = 4
-    AUTO_CLASSES_MIN_DEGREE = 2.0
+    AUTO_CLASSES = AUTO_CLASSES
+    AUTO_CLASSES_MIN_DEGREE = AUTO_CLASSES_MIN_DEGREE
 
     def auto_classes(self, B: int) -> int:
         """Classes for the engine's own plan of B workgroups: AUTO_CLASSES for
         the linear kernel when an item meets at least AUTO_CLASSES_MIN_DEGREE
         ratings per user range of the one-class plan, else 1."""
-        if self.kernel != "linear" or self.n == 0 or B < 1:
-            return 1
-        deg = self.n / float(max(self.n_items, 1) * B)
-        return self.AUTO_CLASSES if deg >= self.AUTO_CLASSES_MIN_DEGREE else 1
+        return auto_strata_classes(self.kernel, self.n, self.n_items, B)
 
     def _l2_handoff_fits(self) -> bool:
         """MF_FLAG_L2_HANDOFF by the plan (env MF_STRATA_L2=0 / 1 forces it

@@ -108,10 +108,10 @@ class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
         if type in ("fit", "update"):
             ids = self._int64_ids(X)
             if ids is not None:
-                perm = self._checked_permutation(ids)
+                perm, dense = self._checked_permutation(ids, dense=type == "fit")
                 rating = _aligned_rating(X, y) if type == "fit" else None
                 if rating is not None:
-                    return self._fit_maps_native(X.index, ids, rating, perm)
+                    return self._fit_maps_native(X.index, ids, rating, perm, dense)
                 native = perm
 
         X = X.loc[:, ["user_id", "item_id"]]
@@ -121,7 +121,8 @@ class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
         if type in ("fit", "update"):
             if native is not None:
                 if type == "fit":
-                    return self._fit_maps_native(X.index, ids, X["rating"].to_numpy(), native)
+                    return self._fit_maps_native(X.index, ids, X["rating"].to_numpy(), native,
+                                                 dense)
                 X = X.iloc[native]
             else:
                 if X.duplicated(subset=["user_id", "item_id"]).sum() != 0:
@@ -173,41 +174,48 @@ class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
         return None if u is None or i is None else (u, i)
 
     @staticmethod
-    def _checked_permutation(ids) -> np.ndarray:
-        """The duplicate-pair check (recommender_base.py:125-128) on worker
-        threads beside ``X.sample(frac=1)``'s draw (:131) on this one; if the
-        check fails, the RNG state is restored before the ValueError."""
+    def _checked_permutation(ids, dense: bool = False):
+        """(perm, dense ids or None): the duplicate-pair check
+        (recommender_base.py:125-128) -- and with ``dense`` the columns'
+        ``_prep.dense_ids`` -- on worker threads beside ``X.sample(frac=1)``'s
+        draw (:131) on this one; if the check fails, the RNG state is
+        restored before the ValueError."""
         state = np.random.get_state()
-        with ThreadPoolExecutor(1) as ex:
+        with ThreadPoolExecutor(3 if dense else 1) as ex:
             dup = ex.submit(_prep.pairs_duplicated, *ids)
+            dn = [ex.submit(_prep.dense_ids, v) for v in ids] if dense else None
             perm = _prep.legacy_permutation(len(ids[0]))       # = X.sample's draw
             if dup.result():
                 np.random.set_state(state)
                 raise ValueError("Duplicate user-item ratings in matrix")
-        return perm
+            dn = [f.result() for f in dn] if dense else None
+        return perm, dn
 
     def _fit_maps_native(self, index: pd.Index, ids, rating: np.ndarray,
-                         perm: np.ndarray) -> pd.DataFrame:
+                         perm: np.ndarray, dense=None) -> pd.DataFrame:
         """The fit branch for integer ids: the rows in ``perm`` order (the
         order X.sample(frac=1) gives), id maps in first-appearance order of
         that order (pd.factorize / unique of the shuffled column), all in
-        mf_prep.cpp (users and items on two threads)."""
-
-        def one(v):
-            c, uniq = _prep.factorize(_prep.gather(v, perm))
-            return c, uniq
-
-        with ThreadPoolExecutor(2) as ex:
-            res = list(ex.map(one, ids))
-        maps = []
-        codes = []
-        for (c, uniq), dt in zip(res, self._id_dtypes):
-            uniq = uniq.view(dt) if dt.itemsize == 8 else uniq.astype(dt)
-            maps.append(dict(zip(uniq, range(len(uniq)))))
-            codes.append(c)
+        mf_prep.cpp: from the columns' dense ids (``dense``, drawn beside the
+        permutation, or here), users, items and the ratings on three threads;
+        this one builds each id map as soon as its column is done."""
+        if dense is None:
+            dense = [_prep.dense_ids(v) for v in ids]
+        with ThreadPoolExecutor(3) as ex:
+            # items first: their map is small and is built while the users finish
+            fut = [ex.submit(_prep.factorize_shuffled, d, perm) for d in dense[::-1]][::-1]
+            num = rating.dtype.kind in "fiu"
+            rfut = ex.submit(_prep.gather, rating, perm) if num else None
+            maps, codes = [None, None], [None, None]
+            for k in (1, 0):
+                c, uniq = fut[k].result()
+                dt = self._id_dtypes[k]
+                uniq = uniq.view(dt) if dt.itemsize == 8 else uniq.astype(dt)
+                maps[k] = dict(zip(uniq, range(len(uniq))))
+                codes[k] = c
+            rating = rfut.result() if num else rating[perm]
         self.user_id_map, self.item_id_map = maps
         self.n_users, self.n_items = len(maps[0]), len(maps[1])
-        rating = _prep.gather(rating, perm) if rating.dtype.kind in "fiu" else rating[perm]
         idx = index
         if isinstance(idx, pd.RangeIndex):
             idx = pd.Index(idx.start + idx.step * perm if (idx.start, idx.step) != (0, 1)

@@ -330,6 +330,7 @@ def _simulate_fit(world, blocks=None):
     RandomState([draw, r]); replica = start + sum of the rank deltas."""
     import matrix_factorization as mf
     from matrix_factorization.distributed import local_shard, shard_users
+    from matrix_factorization.engine import stratum_order
 
     X, y = _frame()
     np.random.seed(SEED)
@@ -348,9 +349,13 @@ def _simulate_fit(world, blocks=None):
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         e = CpuEngine(lu, li, lr_, hi - lo, m.n_items, K, mu)
         e.load_params(P=P[lo:hi], bu=np.zeros(hi - lo), Q=Q, bi=np.zeros(m.n_items))
-        if blocks == "auto":            # the GPU engine's own choice of B
-            from matrix_factorization.engine import choose_strata_blocks
-            e.prepare_strata(choose_strata_blocks(lu, li, hi - lo, m.n_items, K, 1)[0])
+        if blocks == "auto":            # the GPU engine's own choice of B and classes
+            from matrix_factorization.engine import auto_strata_classes, choose_strata_blocks
+            B = choose_strata_blocks(lu, li, hi - lo, m.n_items, K, 1)[0]
+            C = auto_strata_classes("linear", len(lu), m.n_items, B)
+            if C > 1:
+                B = choose_strata_blocks(lu, li, hi - lo, m.n_items, K, 1, classes=C)[0]
+            e.prepare_strata(B, classes=C)
         else:
             e.prepare_strata(blocks)
         engs.append(e)
@@ -363,7 +368,7 @@ def _simulate_fit(world, blocks=None):
             e.Q = torch.as_tensor(Q.copy())
             e.bi = torch.as_tensor(bi.copy())
             rs = np.random.RandomState([draw, rank])
-            seq = rs.permutation(e.strata.B)
+            seq = stratum_order(rs, e.strata)
             e.epoch_strata(seq, int(rs.randint(0, 2**31 - 1)), LR, REG)
             dQ += e.Q.numpy() - Q
             dbi += e.bi.numpy() - bi

@@ -76,6 +76,29 @@ def test_factorize_is_pandas(n, hi):
     assert np.array_equal(c, c2) and np.array_equal(u, u2)
 
 
+@pytest.mark.parametrize("n,lo,hi", [(0, 0, 5), (1, 7, 8), (10, -3, 3), (5000, 0, 40),
+                                     (200_000, -10**15, 10**15), (300_000, 0, 2**62),
+                                     (1_000_000, 1000, 1700), (400_000, 0, 2_000_000)])
+def test_factorize_shuffled_is_pandas(n, lo, hi):
+    """dense ids of the unshuffled column (direct range or hashed) +
+    first appearance in perm order == pd.factorize(v[perm])."""
+    rs = np.random.RandomState(n % 997)
+    v = rs.randint(lo, hi, n).astype(np.int64)
+    perm = rs.permutation(n).astype(np.int64)
+    dn = _prep.dense_ids(v)
+    direct = dn[3] is None
+    assert direct == (n > 0 and hi - lo <= n + _prep.DIRECT_SPAN_SLACK)
+    c, u = _prep.factorize_shuffled(dn, perm)
+    c2, u2 = pd.factorize(v[perm], sort=False)
+    assert np.array_equal(c, c2) and np.array_equal(u, u2)
+
+
+def test_first_appearance_rejects_bad_permutation():
+    v = np.arange(10, dtype=np.int64)
+    with pytest.raises(_lib.MFLibraryError):
+        _prep.factorize_shuffled(_prep.dense_ids(v), np.full(10, 10, np.int64))
+
+
 @pytest.mark.parametrize("n", [0, 1, 2, 1000, 300_000])
 def test_pairs_duplicated_is_pandas(n):
     rs = np.random.RandomState(n)

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--workload", default="c2")
     ap.add_argument("--blocks", type=int, default=None)
     ap.add_argument("--rotate", type=int, default=0)
+    ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--classes", default="auto", help="user-range classes: auto or 1..4")
     args = ap.parse_args()
     nu, ni, nnz, k, kernel, _ = bench.WORKLOADS[args.workload]
     u, i, r = bench.synth(nu, ni, nnz)
@@ -38,15 +40,17 @@ def main():
         ilo = item_ranges(i, ni, args.rotate)
         u, i, r = local_shard(u, i, r, bounds, 0)
         nu = int(bounds[1])
-    eng = SGDEngine(u, i, r, nu, ni, k, kernel, "float32", "cuda:0", gamma=1.0 / k,
+    dt = np.float64 if args.dtype == "float64" else np.float32
+    eng = SGDEngine(u, i, r, nu, ni, k, kernel, args.dtype, "cuda:0", gamma=1.0 / k,
                     min_rating=1, max_rating=5, global_mean=mu)
+    eng.strata_classes = args.classes if args.classes == "auto" else int(args.classes)
     plan = eng.prepare_strata(n_blocks=args.blocks,
                               item_bounds=ilo if args.rotate else None)
     B = plan.B
     rs = np.random.RandomState(0)
-    eng.load_params(rs.normal(0, 0.1, (nu, k)).astype(np.float32),
-                    rs.normal(0, 0.1, (ni, k)).astype(np.float32),
-                    np.zeros(nu, np.float32), np.zeros(ni, np.float32))
+    eng.load_params(rs.normal(0, 0.1, (nu, k)).astype(dt),
+                    rs.normal(0, 0.1, (ni, k)).astype(dt),
+                    np.zeros(nu, dt), np.zeros(ni, dt))
 
     def run(seq, seed):
         if args.rotate:
@@ -77,7 +81,9 @@ def main():
     sig = st[:, :, 3] - st[:, :, 2]
     gap = st[1:, :, 0] - st[:-1, :, 3]
     span = st[:, :, 3].max() - st[:, :, 0].min()
-    pl0 = plan.phases[0] if args.rotate else plan
+    # the probe keeps the stamps of the last launch: phase 0 of the rotation,
+    # the last item phase of a phased plan
+    pl0 = plan.phases[0] if args.rotate else (plan.phases[-1] if hasattr(plan, "phases") else plan)
     steps = np.diff(pl0.bstep).reshape(NSQ, B)           # [s, w]
     print(f"{args.workload}{' rotate N=%d sub-epoch' % args.rotate if args.rotate else ''}: "
           f"B={B} C={plan.classes} NS={plan.NS} epoch kernel {t0.elapsed_time(t1):.3f} ms, "
