@@ -80,6 +80,10 @@ enum {
                                  whole number of 128-B lines and a 128-B aligned
                                  P; ignored otherwise (and with user-range
                                  classes C > 1). */
+    MF_FLAG_NO_EARLY_POLL = 512, /* with MF_FLAG_PERSISTENT and classes C > 1: wait
+                                 for each position's user range at its start
+                                 instead of polling it once during the previous
+                                 block (diagnostic A/B) */
     /* mf_sgd_epoch_strata: bits 24..27 = C - 1, the plan's user-range classes
        (mf_strata_plan_build_classes; 0 = C = 1, the plain B x B plan) */
     MF_FLAG_CLASSES_SHIFT = 24

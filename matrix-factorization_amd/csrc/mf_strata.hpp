@@ -86,6 +86,8 @@ struct StrataArgs {
     Hyper<T> h;
     int64_t* probe;          // nullable: persistent-kernel phase stamps (mf_strata_set_probe)
     int32_t* xtab;           // nullable: MF_FLAG_L2_HANDOFF -- per workgroup ((base+1) << 4) | XCC id
+    int32_t early;           // persistent, C > 1: poll the next position's user range during
+                             // the current block (0: MF_FLAG_NO_EARLY_POLL)
 };
 
 // first step of block `blk` in this epoch (mirrored by engine.strata_mix)
@@ -125,11 +127,18 @@ __device__ __forceinline__ void lds_barrier() {
 // t+2 in flight while step t applies; 2: rows of t+1 and t+2, triples of t+3
 // and t+4 -- for blocks of few steps, where each step otherwise waits one
 // load latency).
+// hook(): called once the prologue's loads are issued and consumed, before
+// the first step (vmcnt counts in issue order: a load issued ahead of the
+// prologue would hold up its waits).
+struct StrataNoHook {
+    __device__ __forceinline__ void operator()() const {}
+};
 template <typename T, int W, int GS, int V, int KERN, int S, bool WT = false, bool BUS_IN = false,
-          int DEPTH = 1, int NW = kStrataWaves>
+          int DEPTH = 1, int NW = kStrataWaves, typename Hook = StrataNoHook>
 __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk, int ulo, int ilo,
                                              T* Qs, T* Bis, T* Bus, const Hyper<T> h,
-                                             int nus = 0, bool keep_l2 = false) {
+                                             int nus = 0, bool keep_l2 = false,
+                                             const Hook& hook = Hook{}) {
     using VT = typename VecOf<T, W>::type;
     constexpr int R = kWave / GS;
     constexpr int RPW = S * R;
@@ -422,6 +431,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
             Bus[x] = buf_ld<16, T>(brs, (uint32_t)(ulo + x) * (uint32_t)sizeof(T));
         lds_barrier();
     }
+    hook();
     // Whole unrolled groups inside the loop, the remainder after it: a group
     // cut short inside the loop body would give the compiler a back-edge on
     // which a prefetched row is never consumed, and it then drains every
@@ -599,7 +609,7 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
                                                                     int32_t* err) {
     constexpr int TH = NW * kWave;
     extern __shared__ __align__(16) unsigned char smem[];
-    __shared__ int s_abort, s_base, s_l2ok;
+    __shared__ int s_abort, s_base, s_l2ok, s_next;
     const int B = A.B;
     const int w = blockIdx.x;
     const int ilo = A.ibnd[w], nqi = A.ibnd[w + 1] - ilo;
@@ -683,62 +693,113 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
         l2ok = s_l2ok != 0;
     }
     const int C = A.cls;
+    // Early poll (C > 1): the next position's user range was released C - 1
+    // blocks before it is needed, so its holder's counter is read ONCE,
+    // during the current block (issued after the block's prologue, read at
+    // its end); when that shows the range released, the next position starts
+    // without the poll's round trip and its barrier.  The next position's
+    // geometry (scalar loads) is read beside the current block's drain.
+    const __amdgpu_buffer_rsrc_t drs = buf_rsrc(done, (uint64_t)B * sizeof(int32_t));
+    // position geometry: stratum, user range, and the workgroup that held the
+    // range C positions back (scalar loads; each position's are issued two
+    // positions ahead, inside a block, so no wait at a block boundary meets
+    // them)
+    struct Geo { int s, ulo, nus, wd; };
+    auto geo = [&](int t) __attribute__((always_inline)) {
+        Geo g;
+        g.s = seq.s[t];
+        const int ub = (g.s + C * w) % (C * B);
+        g.ulo = A.ubnd[ub];
+        g.nus = A.ubnd[ub + 1] - g.ulo;
+        g.wd = t >= C ? (w + g.s / C - (int)seq.s[t - C] / C + 2 * B) % B : 0;
+        return g;
+    };
+    Geo gc = geo(0);
+    Geo gn = n_seq > 1 ? geo(1) : gc;
+    bool ready = false;                  // position t's range seen released (uniform)
     for (int t = 0; t < n_seq; ++t) {
-        const int s = seq.s[t];
-        const int ub = (s + C * w) % (C * B);
-        const int ulo = A.ubnd[ub], nus = A.ubnd[ub + 1] - ulo;
         stamp(t, 0);
-        if (threadIdx.x == 0) {
-            int ab = 0;
-            if (t >= C) {
-                // the user range's previous holder: same class, C positions back
-                const int wd = (w + s / C - (int)seq.s[t - C] / C + 2 * B) % B;
-                int64_t spins = 0;
-                while (__hip_atomic_load(done + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
-                       base + t - C + 1) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins > kStrataSpinLimit ||
-                        __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-                        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        ab = 1;
-                        break;
+        if (!ready) {
+            if (threadIdx.x == 0) {
+                int ab = 0;
+                if (t >= C) {
+                    // the user range's previous holder: same class, C positions back
+                    int64_t spins = 0;
+                    while (__hip_atomic_load(done + gc.wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                           base + t - C + 1) {
+                        __builtin_amdgcn_s_sleep(2);
+                        if (++spins > kStrataSpinLimit ||
+                            __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            ab = 1;
+                            break;
+                        }
                     }
+                    // every load of handed-off bytes below is sc1: no L1 invalidate,
+                    // only keep the compiler from hoisting them above the poll
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 }
-                // every load of handed-off bytes below is sc1: no L1 invalidate,
-                // only keep the compiler from hoisting them above the poll
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                s_abort = ab;
             }
-            s_abort = ab;
+            __syncthreads();
+            if (s_abort) return;
         }
-        __syncthreads();
-        if (s_abort) return;
         stamp(t, 1);
+        const bool more = t + 1 < n_seq;
+        // the early poll: one sc1 buffer load of the next range's holder's
+        // counter, every lane the same word, dropped (no access) when unused
+        const bool ep = A.early && more && C > 1 && t + 1 >= C;
+        int poll = 0;
+        Geo g2 = gn;
+        auto hook = [&]() __attribute__((always_inline)) {
+            poll = buf_ld<16, int>(drs, ep ? (uint32_t)gn.wd * (uint32_t)sizeof(int32_t) : kBufDrop);
+            if (t + 2 < n_seq) g2 = geo(t + 2);
+        };
         // the user-bias slice is staged inside the block, behind its prologue
         // the next holder of this user range, w + s_t - s_{t+1}, on this XCD
         // (same residue mod 8, B a multiple of 8): rows stored plainly stay
         // in the L2 it reads; otherwise write-through, as always
-        const bool keep = l2ok && t + 1 < n_seq && ((s - (int)seq.s[t + 1]) & 7) == 0;
-        strata_block<T, W, GS, V, KERN, S, true, true, DEPTH, NW>(A, (int64_t)s * B + w, ulo, ilo, Qs,
-                                                              Bis, Bus, h, nus, keep);
+        const bool keep = l2ok && more && ((gc.s - gn.s) & 7) == 0;
+        strata_block<T, W, GS, V, KERN, S, true, true, DEPTH, NW>(A, (int64_t)gc.s * B + w, gc.ulo, ilo,
+                                                              Qs, Bis, Bus, h, gc.nus, keep, hook);
+        // lane 0 decides for the workgroup (the barrier below publishes it);
+        // every wave's loads of the next range come after that barrier
+        if (threadIdx.x == 0)
+            s_next = A.early && more && C > 1 && (t + 1 < C || poll >= base + t + 2 - C);
         __syncthreads();
         stamp(t, 2);
+        const bool rdy = s_next != 0;
         if constexpr (KERN != MF_RBF) {
             if (A.upd_user)
-                for (int x = threadIdx.x; x < nus; x += TH)
-                    __hip_atomic_store(A.Bu + ulo + x, Bus[x], __ATOMIC_RELAXED,
+                for (int x = threadIdx.x; x < gc.nus; x += TH)
+                    __hip_atomic_store(A.Bu + gc.ulo + x, Bus[x], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);     // write-through
         }
         // every storing wave drains its write-through stores, then one lane
-        // signals (no L2 write-back fence: nothing handed off sits dirty in L2)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            // L2 hand-offs: rows of this range stored plainly by earlier blocks
-            // on this XCD must reach memory before another XCD reads them
-            if (l2ok && !keep && t + 1 < n_seq) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __hip_atomic_store(done + w, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // signals (no L2 write-back fence: nothing handed off sits dirty in L2).
+        // With C > 1 a range's next holder comes C positions later, so the
+        // drain and the signal are taken every D = C - 1 positions (and at the
+        // last): the counter then jumps by D, each range is published at most
+        // D - 1 blocks late, i.e. still before its next holder's position --
+        // D - 1 of every D drains off the chain.  In between, a barrier only
+        // (the next block rewrites the bias slice the stores above read).
+        const int D = C > 1 ? C - 1 : 1;
+        if (!more || t % D == D - 1) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                // L2 hand-offs: rows of this range stored plainly by earlier blocks
+                // on this XCD must reach memory before another XCD reads them
+                if (l2ok && !keep && more) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                __hip_atomic_store(done + w, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else {
+            __syncthreads();
         }
         stamp(t, 3);
+        ready = rdy;
+        gc = gn;
+        gn = g2;
     }
     __syncthreads();
     if (A.Dq)
@@ -945,6 +1006,7 @@ struct StrataRun {
         a.h = make_hyper<T>(p.mu, p.lr, p.reg, p.gamma, p.lo, p.hi);
         a.probe = strata_probe_ptr();
         a.xtab = nullptr;
+        a.early = (p.flags & MF_FLAG_NO_EARLY_POLL) ? 0 : 1;
         hipEvent_t ev[2] = {nullptr, nullptr};
         if (p.kernel_ms) {
             MF_HIP_CHECK(hipEventCreate(&ev[0]));

@@ -958,6 +958,8 @@ class SGDEngine:
             flags |= _lib.MF_FLAG_DEEP_PIPE
         if os.environ.get("MF_STRATA_COOP") == "0" or _under_rocprofiler():
             flags |= _lib.MF_FLAG_NO_COOP
+        if os.environ.get("MF_STRATA_EARLY") == "0":
+            flags |= _lib.MF_FLAG_NO_EARLY_POLL
         if pl.narrow:
             flags |= _lib.MF_FLAG_NARROW
         flags |= (pl.classes - 1) << _lib.MF_FLAG_CLASSES_SHIFT
