@@ -899,6 +899,8 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
                        else f"strata (B={B}: {nb} launches/epoch, ")
                       + (f"{cls} user-range classes ({cls * B} user ranges, {cls - 1} "
                          f"block(s) of slack per hand-off), " if cls > 1 else "")
+                      + (f"{1 + len(eng._regroups)} relabelled plans, one drawn per epoch, "
+                         if eng._regroups else "")
                       + "item slabs in LDS, "
                       f"{plan.NS} user-owned slots "
                       f"({256 if plan.narrow else plan.NS * 1024 // strata_slots(k, eng.dcode)} "
@@ -967,7 +969,7 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
 
     def serial(ep, seq):
         if strata:
-            return plan.serial_order(seq, rot_for(ep)).astype(np.int64)
+            return eng.serial_order(seq, rot_for(ep)).astype(np.int64)
         return np.concatenate([np.arange(eng.colored[b], eng.colored[b + 1])
                                for b in seq]).astype(np.int64)
 

@@ -507,7 +507,7 @@ class SGDEngine:
                  n_users: int, n_items: int, n_factors: int, kernel: str,
                  dtype="float64", device=None, gamma: float = 0.0,
                  min_rating: float = 0.0, max_rating: float = 5.0,
-                 global_mean: float = 0.0):
+                 global_mean: float = 0.0, eval_order: bool = True):
         self.dev = resolve_device(device)
         self.dtype = canonical_dtype(dtype)
         self.tdt, self.ndt, self.dcode = DTYPES[self.dtype]
@@ -534,9 +534,13 @@ class SGDEngine:
                        or self.i_host.min() < 0 or self.i_host.max() >= n_items):
             raise ValueError("rating ids outside [0, n_users) x [0, n_items)")
         self._upload_triples(self.u_host, self.i_host, self.r_host)
-        self._build_eval()
+        if eval_order:
+            self._build_eval()
+        else:                        # a regrouping's engine: sweeps only, no RMSE pass
+            self.eu, self.ei, self.er, self.eval_offs = self.u, self.i, self.r, None
         self.colored = None          # (offsets,) once prepare_colored() ran
         self.strata = None           # StrataPlan once prepare_strata() ran
+        self._regroups = []          # relabelled plans: [(engine, user perm, item perm)]
         ws = max(_lib.load().mf_sse_workspace_bytes(self.n), 8)
         self.ws = torch.empty((ws + 7) // 8, dtype=torch.float64, device=self.dev)
         self.sse_buf = torch.zeros(16, dtype=torch.float64, device=self.dev)
@@ -728,7 +732,77 @@ class SGDEngine:
             if auto_l2:
                 plan.l2_handoff, plan.order = True, "xcd"
         self.strata = plan
+        K = self._regroup_count(plan)
+        for j in range(1, K):
+            self._build_regroup(j, plan, waves)
         return plan
+
+    # relabelled plans, "regroupings" (DESIGN.md section 3.1): K - 1 more
+    # plans of the same B and classes over randomly relabelled users and
+    # items; every epoch's rotation seed picks one, so which users share a
+    # range and which items share a slab is re-drawn epoch to epoch.  C3,
+    # 4 classes, 20 epochs: train RMSE +1.18e-5 over the reference's mean
+    # with one plan (3.6 SE), +0.73e-5 with two (2.1 SE), +0.79e-5 with four
+    # (profiles/r04/seed_spread_c3_20ep_regroup_r04q.json).  "auto" = 2 for
+    # the linear kernel's multi-class plans (the order-bias regime), else 1;
+    # env MF_STRATA_REGROUP overrides.
+    strata_regroup = "auto"
+    REGROUP_AUTO = 2
+    REGROUP_MAX = 4
+    REGROUP_SEED = 0x5EED
+
+    def _regroup_count(self, plan) -> int:
+        k = os.environ.get("MF_STRATA_REGROUP", self.strata_regroup)
+        if k in (None, "auto"):
+            return (self.REGROUP_AUTO if plan.classes > 1 and self.kernel == "linear"
+                    and self.n > 0 else 1)
+        k = int(k)
+        if not 1 <= k <= self.REGROUP_MAX:
+            raise ValueError(f"strata regroupings must be in [1, {self.REGROUP_MAX}], got {k}")
+        return k
+
+    def _build_regroup(self, j: int, plan, waves) -> None:
+        """Regrouping j: an engine over relabelled ids (user x -> pu[x], item
+        y -> pi[y]) with a plan of the same B, classes and phases; it shares
+        this engine's persistent-sweep workspace (position counters, error
+        word), so failure detection and recovery see its launches too."""
+        rs = np.random.RandomState(self.REGROUP_SEED + j)
+        pu = torch.from_numpy(rs.permutation(self.n_users).astype(np.int64)).to(self.dev)
+        pi = torch.from_numpy(rs.permutation(self.n_items).astype(np.int64)).to(self.dev)
+        uj = pu.index_select(0, self.u.long()).to(torch.int32).cpu().numpy()
+        ij = pi.index_select(0, self.i.long()).to(torch.int32).cpu().numpy()
+        e = SGDEngine(uj, ij, self.r_host, self.n_users, self.n_items, self.k, self.kernel,
+                      self.dtype, self.dev, self.gamma, self.min_rating, self.max_rating,
+                      self.global_mean, eval_order=False)
+        del uj, ij
+        e.strata_persistent = self.strata_persistent
+        e.strata_deep_pipe = self.strata_deep_pipe
+        e.strata_regroup = 1
+        if waves is None:
+            waves = 16 if plan.NS == strata_slots(self.k, self.dcode, 16) else 8
+            if getattr(plan, "narrow", False):
+                waves = 4
+        phases = len(plan.phases) if isinstance(plan, PhasedStrata) else None
+        e.prepare_strata(n_blocks=plan.B, waves=waves, phases=phases, classes=plan.classes)
+        if e.strata.n_strata != plan.n_strata:
+            raise RuntimeError("regrouped plan differs in strata count")
+        self._regroups.append((e, pu, pi))
+
+    def _regroup_pick(self, seed: int) -> int:
+        """Which plan runs the epoch with rotation seed ``seed`` (0 = this
+        engine's own): a hash of the seed, so replays pick the same."""
+        K = 1 + len(self._regroups)
+        if K == 1:
+            return 0
+        return int((((int(seed) & 0xFFFFFFFF) * 2654435761) & 0xFFFFFFFF) >> 16) % K
+
+    def serial_order(self, seq, seed) -> np.ndarray:
+        """The rating indices in the order the strata epoch (seq, seed)
+        applies them, whichever plan it picks (indices into this engine's
+        rating arrays; a regrouping lists the same ratings)."""
+        j = self._regroup_pick(seed)
+        pl = self.strata if j == 0 else self._regroups[j - 1][0].strata
+        return pl.serial_order(seq, seed)
 
     # the automatic choice of user-range classes (DESIGN.md section 3): the
     # strata order trains measurably slower than the reference's random order
@@ -941,6 +1015,10 @@ class SGDEngine:
             raise RuntimeError("call prepare_strata() first")
         seq = (np.arange(pl.n_strata, dtype=np.int32) if seq is None
                else np.ascontiguousarray(seq, np.int32))
+        j = self._regroup_pick(seed) if delta is None else 0
+        if j > 0:
+            return self._epoch_regroup(j - 1, seq, seed, lr, reg, update_user, update_item,
+                                       timing, persistent)
         if isinstance(pl, PhasedStrata):
             return self._epoch_phased(pl, seq, seed, lr, reg, update_user, update_item, timing,
                                       persistent, delta)
@@ -949,6 +1027,47 @@ class SGDEngine:
         self._run_strata(pl, seq, seed, lr, reg, update_user, update_item, flags, ms, delta,
                          self.Q, self.bi, self.n_items)
         return (ms[0], int(ms[1])) if timing else None
+
+    def _epoch_regroup(self, j, seq, seed, lr, reg, update_user, update_item, timing,
+                       persistent):
+        """One epoch on regrouping j: the parameters are gathered into its
+        labelling, swept there, and gathered back (device index copies)."""
+        e, pu, pi = self._regroups[j]
+        e.global_mean, e.gamma = self.global_mean, self.gamma
+        e.min_rating, e.max_rating = self.min_rating, self.max_rating
+        if e.P is None or e.P.shape != self.P.shape:
+            e.load_params(P=torch.zeros_like(self.P), Q=torch.zeros_like(self.Q),
+                          bu=None if self.bu is None else torch.zeros_like(self.bu),
+                          bi=None if self.bi is None else torch.zeros_like(self.bi))
+        e.P.index_copy_(0, pu, self.P)
+        e.Q.index_copy_(0, pi, self.Q)
+        if self.bu is not None:
+            e.bu.index_copy_(0, pu, self.bu)
+        if self.bi is not None:
+            e.bi.index_copy_(0, pi, self.bi)
+        self._ensure_strata_ws(e.strata.B, len(seq))
+        e._strata_ws = self._strata_ws           # shared counters and error word
+        out = e.epoch_strata(seq, seed, lr, reg, update_user, update_item, timing, persistent)
+        torch.index_select(e.P, 0, pu, out=self.P)
+        torch.index_select(e.Q, 0, pi, out=self.Q)
+        if self.bu is not None:
+            torch.index_select(e.bu, 0, pu, out=self.bu)
+        if self.bi is not None:
+            torch.index_select(e.bi, 0, pi, out=self.bi)
+        return out
+
+    def _ensure_strata_ws(self, B: int, n_seq: int) -> None:
+        wsb = int(_lib.load().mf_strata_workspace_bytes(B, n_seq))
+        old = getattr(self, "_strata_ws", None)
+        if old is None or old.numel() * 4 < wsb:
+            # zeroed once: the error flag (int32 at index B) is sticky until
+            # check_strata() raises or clear_strata_error() resets it, and
+            # the position counters done[0:B] grow across launches; a grown
+            # workspace carries both over
+            ws = torch.zeros((wsb + 3) // 4, dtype=torch.int32, device=self.dev)
+            if old is not None:
+                ws[: B + 1] = old[: B + 1]
+            self._strata_ws = ws
 
     def _strata_flags(self, pl, persistent):
         if persistent is None:
@@ -1013,17 +1132,7 @@ class SGDEngine:
 
     def _run_strata(self, pl, seq, seed, lr, reg, update_user, update_item, flags, ms, delta,
                     Q, bi, n_items):
-        wsb = int(_lib.load().mf_strata_workspace_bytes(pl.B, len(seq)))
-        old = getattr(self, "_strata_ws", None)
-        if old is None or old.numel() * 4 < wsb:
-            # zeroed once: the error flag (int32 at index B) is sticky until
-            # check_strata() raises or clear_strata_error() resets it, and
-            # the position counters done[0:B] grow across launches; a grown
-            # workspace carries both over
-            ws = torch.zeros((wsb + 3) // 4, dtype=torch.int32, device=self.dev)
-            if old is not None:
-                ws[: pl.B + 1] = old[: pl.B + 1]
-            self._strata_ws = ws
+        self._ensure_strata_ws(pl.B, len(seq))
         args = (_tp(pl.d_u), _tp(pl.d_i), _tp(pl.d_r),
                 pl.n_positions, pl.B, _tp(pl.d_ubnd), _tp(pl.d_ibnd), _tp(pl.d_bstep),
                 pl.NS, pl.max_items, pl.max_users, _np(seq), len(seq),

@@ -27,6 +27,10 @@ Three keyword arguments are new and default to the reference's behaviour:
               >= 2 ratings per user range and block, else 1 -- the order
               then trains like the reference's random order, DESIGN.md
               section 3) or 1..4 (1: the fastest plan).
+``strata_regroup``  schedule "strata" only: relabelled plans drawn epoch by
+              epoch (which users share a range, which items a slab),
+              "auto" (default: 2 for the linear kernel's multi-class plans,
+              else 1) or 1..4.
 ``exchange``  process-group mode only: "rotate" (default; exact -- items are
               cut into one range per rank and the ranges are passed round the
               ring between sub-epochs, so every rating is applied with the
@@ -100,7 +104,7 @@ class KernelMF(RecommenderBase):
                  init_sd: float = 0.1, min_rating: int = 0, max_rating: int = 5,
                  verbose: int = 1, dtype: str = "float64",
                  schedule: str = "exact", device=None, distributed: bool = False,
-                 exchange: str = "rotate", strata_classes="auto"):
+                 exchange: str = "rotate", strata_classes="auto", strata_regroup="auto"):
         if kernel not in ("linear", "sigmoid", "rbf"):
             raise ValueError("Kernel must be one of linear, sigmoid, or rbf")
         if schedule not in ("exact", "colored", "strata"):
@@ -109,6 +113,8 @@ class KernelMF(RecommenderBase):
             raise ValueError(f"exchange must be one of {EXCHANGES}")
         if strata_classes != "auto" and strata_classes not in (1, 2, 3, 4):
             raise ValueError("strata_classes must be 'auto' or 1..4")
+        if strata_regroup != "auto" and strata_regroup not in (1, 2, 3, 4):
+            raise ValueError("strata_regroup must be 'auto' or 1..4")
         canonical_dtype(dtype)
         super().__init__(min_rating=min_rating, max_rating=max_rating, verbose=verbose)
         self.n_factors = n_factors
@@ -126,6 +132,7 @@ class KernelMF(RecommenderBase):
         self.distributed = distributed
         self.exchange = exchange
         self.strata_classes = strata_classes
+        self.strata_regroup = strata_regroup
 
     # ----------------------------------------------------- device state
     def _make_engine(self, X: pd.DataFrame, n_users: int, n_items: int,
@@ -142,6 +149,7 @@ class KernelMF(RecommenderBase):
                         gamma=self.gamma, min_rating=self.min_rating,
                         max_rating=self.max_rating, global_mean=self.global_mean)
         eng.strata_classes = getattr(self, "strata_classes", "auto")
+        eng.strata_regroup = getattr(self, "strata_regroup", "auto")
         if schedule == "strata" and n:
             eng.prepare_strata()
         elif schedule == "colored" and n:
@@ -208,7 +216,7 @@ class KernelMF(RecommenderBase):
         # defaults (the reference's pickles have none of them)
         for key, default in (("dtype", "float64"), ("schedule", "exact"), ("device", None),
                              ("distributed", False), ("exchange", "rotate"),
-                             ("strata_classes", "auto")):
+                             ("strata_classes", "auto"), ("strata_regroup", "auto")):
             state.setdefault(key, default)
         self.__dict__.update(state)
         _warn_if_no_device()

@@ -484,7 +484,7 @@ def test_user_range_classes(dtype, kernel, k, B, C, waves, phases):
     hyp = dict(kernel=kernel, gamma=1.0 / k, min_rating=1.0, max_rating=5.0)
     P2, Q2, bu2, bi2 = P0.copy(), Q0.copy(), bu0.copy(), bi0.copy()
     for seq, seed in eps:
-        order = plan.serial_order(seq, seed)
+        order = eng.serial_order(seq, seed)        # the plan the epoch picked
         assert np.array_equal(np.sort(order), np.arange(nnz))
         oracle.sgd_pass(eng.u_host, eng.i_host, eng.r_host.astype(np.float64), eng.global_mean,
                         bu2, bi2, P2, Q2, lr=0.01, reg=0.02, order=order, **hyp)
@@ -502,3 +502,57 @@ def test_user_range_classes(dtype, kernel, k, B, C, waves, phases):
         res.append(eng.params_numpy())
     for a, b in zip(*res):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("dtype,phases,K", [("float64", None, 2), ("float32", None, 3),
+                                           ("float64", 2, 2)])
+def test_regrouped_plans(dtype, phases, K):
+    """Relabelled plans (engine.strata_regroup): every epoch's seed picks one
+    of K plans of the same B and classes over relabelled users / items; the
+    parameters are gathered into its labelling and back, so after each epoch
+    they are the oracle's sweep in the picked plan's serial order
+    (engine.serial_order), with persistent == per-stratum bits, and the
+    auto rule gives the linear kernel's multi-class plans 2."""
+    import oracle
+    from matrix_factorization.engine import stratum_order
+
+    nu, ni, nnz, k, B, C = 2000, 700, 90000, 32, 5, 4
+    u, i, r = _synthetic(93, nu, ni, nnz)
+    rs = np.random.RandomState(94)
+    P0 = rs.normal(0, 0.1, (nu, k)); Q0 = rs.normal(0, 0.1, (ni, k))
+    bu0 = rs.normal(0, 0.1, nu); bi0 = rs.normal(0, 0.1, ni)
+    seeds = [5001, 5002, 5003, 5004, 5005, 5006]
+    out = []
+    for persistent in (True, False):
+        eng = _engine(u, i, r, nu, ni, k, "linear", dtype, P0, Q0, bu0, bi0)
+        eng.strata_regroup = K
+        plan = eng.prepare_strata(n_blocks=B, phases=phases, classes=C)
+        assert len(eng._regroups) == K - 1
+        picks = {eng._regroup_pick(sd) for sd in seeds}
+        assert len(picks) > 1                      # the seeds exercise a regrouping
+        eps = []
+        for ep, sd in enumerate(seeds):
+            seq = stratum_order(np.random.RandomState(ep), plan)
+            eng.epoch_strata(seq, sd, lr=0.01, reg=0.02, persistent=persistent)
+            eps.append((seq, sd))
+        eng.check_strata()
+        out.append(eng.params_numpy())
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    P2, Q2, bu2, bi2 = P0.copy(), Q0.copy(), bu0.copy(), bi0.copy()
+    for seq, sd in eps:
+        order = eng.serial_order(seq, sd)
+        assert np.array_equal(np.sort(order), np.arange(nnz))
+        oracle.sgd_pass(eng.u_host, eng.i_host, eng.r_host.astype(np.float64), eng.global_mean,
+                        bu2, bi2, P2, Q2, lr=0.01, reg=0.02, order=order, kernel="linear",
+                        gamma=1.0 / k, min_rating=1.0, max_rating=5.0)
+    tol = 1e-11 if dtype == "float64" else 1e-4
+    for g, o in zip(out[0], (P2, Q2, bu2, bi2)):
+        _close(g, o, tol)
+    # the automatic rule: 2 plans for the linear kernel's multi-class plans, 1 otherwise
+    e2 = _engine(u, i, r, nu, ni, k, "linear", dtype, P0, Q0, bu0, bi0)
+    e2.prepare_strata(n_blocks=B, classes=C)
+    assert len(e2._regroups) == 1
+    e3 = _engine(u, i, r, nu, ni, k, "linear", dtype, P0, Q0, bu0, bi0)
+    e3.prepare_strata(n_blocks=B, classes=1)
+    assert len(e3._regroups) == 0

@@ -327,6 +327,9 @@ def test_constructor_validation_and_sklearn_clone():
     assert m.strata_classes == "auto" and clone(KernelMF(strata_classes=2)).strata_classes == 2
     with pytest.raises(ValueError, match="strata_classes"):
         KernelMF(strata_classes=5)
+    assert m.strata_regroup == "auto" and clone(KernelMF(strata_regroup=1)).strata_regroup == 1
+    with pytest.raises(ValueError, match="strata_regroup"):
+        KernelMF(strata_regroup=0)
 
 
 def test_auto_classes_rule():
