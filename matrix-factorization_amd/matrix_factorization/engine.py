@@ -24,6 +24,7 @@ Two epoch schedules:
 from __future__ import annotations
 
 import ctypes
+from concurrent.futures import ThreadPoolExecutor
 import math
 import os
 import sys
@@ -723,18 +724,39 @@ class SGDEngine:
                 b8 = self._bounds_for(B8) if B8 >= 2 * XCD_CLASSES else None
                 if b8 is not None:
                     n_blocks, bounds, auto_l2 = B8, b8, True
-        if phases is not None and int(phases) > 1:
-            plan = self._prepare_phased(int(phases), n_blocks, waves, classes=classes)
-        else:
-            plan = self._build_plan(self.u_host, self.i_host, self.n_items, n_blocks, waves,
-                                    bounds, classes)
-            plan.to_device(self.u, self.i, self.r, self.dev)
-            if auto_l2:
-                plan.l2_handoff, plan.order = True, "xcd"
+        # the regroupings' plans (same B, classes and phases) are built on a
+        # worker thread while this one builds the engine's own: the planner
+        # is host code that releases the GIL
+        K = self._regroup_count(classes)
+        worker = None
+        if K > 1 and n_blocks is not None:
+            worker = ThreadPoolExecutor(1)
+            fut = worker.submit(self._build_regroups, K, int(n_blocks), phases, classes, waves)
+        try:
+            if phases is not None and int(phases) > 1:
+                plan = self._prepare_phased(int(phases), n_blocks, waves, classes=classes)
+            else:
+                cums = ((self.degree_cum("user"), self.degree_cum("item"))
+                        if bounds is None and n_blocks is not None else (None, None))
+                plan = self._build_plan(self.u_host, self.i_host, self.n_items, n_blocks, waves,
+                                        bounds, classes, cums)
+                plan.to_device(self.u, self.i, self.r, self.dev)
+                if auto_l2:
+                    plan.l2_handoff, plan.order = True, "xcd"
+        finally:
+            if worker is not None:
+                regroups = fut.result()
+                worker.shutdown()
+        if K > 1 and worker is None:         # B known only now: after the engine's plan
+            regroups = self._build_regroups(
+                K, plan.B, len(plan.phases) if isinstance(plan, PhasedStrata) else None,
+                classes, waves)
+        if K > 1:
+            for e, _, _ in regroups:
+                if e.strata.n_strata != plan.n_strata or e.strata.B != plan.B:
+                    raise RuntimeError("a regrouped plan differs from the engine's in shape")
+            self._regroups = regroups
         self.strata = plan
-        K = self._regroup_count(plan)
-        for j in range(1, K):
-            self._build_regroup(j, plan, waves)
         return plan
 
     # relabelled plans, "regroupings" (DESIGN.md section 3.1): K - 1 more
@@ -751,42 +773,41 @@ class SGDEngine:
     REGROUP_MAX = 4
     REGROUP_SEED = 0x5EED
 
-    def _regroup_count(self, plan) -> int:
+    def _regroup_count(self, classes: int) -> int:
         k = os.environ.get("MF_STRATA_REGROUP", self.strata_regroup)
         if k in (None, "auto"):
-            return (self.REGROUP_AUTO if plan.classes > 1 and self.kernel == "linear"
+            return (self.REGROUP_AUTO if classes > 1 and self.kernel == "linear"
                     and self.n > 0 else 1)
         k = int(k)
         if not 1 <= k <= self.REGROUP_MAX:
             raise ValueError(f"strata regroupings must be in [1, {self.REGROUP_MAX}], got {k}")
         return k
 
-    def _build_regroup(self, j: int, plan, waves) -> None:
-        """Regrouping j: an engine over relabelled ids (user x -> pu[x], item
-        y -> pi[y]) with a plan of the same B, classes and phases; it shares
-        this engine's persistent-sweep workspace (position counters, error
-        word), so failure detection and recovery see its launches too."""
-        rs = np.random.RandomState(self.REGROUP_SEED + j)
-        pu = torch.from_numpy(rs.permutation(self.n_users).astype(np.int64)).to(self.dev)
-        pi = torch.from_numpy(rs.permutation(self.n_items).astype(np.int64)).to(self.dev)
-        uj = pu.index_select(0, self.u.long()).to(torch.int32).cpu().numpy()
-        ij = pi.index_select(0, self.i.long()).to(torch.int32).cpu().numpy()
-        e = SGDEngine(uj, ij, self.r_host, self.n_users, self.n_items, self.k, self.kernel,
-                      self.dtype, self.dev, self.gamma, self.min_rating, self.max_rating,
-                      self.global_mean, eval_order=False)
-        del uj, ij
-        e.strata_persistent = self.strata_persistent
-        e.strata_deep_pipe = self.strata_deep_pipe
-        e.strata_regroup = 1
-        if waves is None:
-            waves = 16 if plan.NS == strata_slots(self.k, self.dcode, 16) else 8
-            if getattr(plan, "narrow", False):
-                waves = 4
-        phases = len(plan.phases) if isinstance(plan, PhasedStrata) else None
-        e.prepare_strata(n_blocks=plan.B, waves=waves, phases=phases, classes=plan.classes)
-        if e.strata.n_strata != plan.n_strata:
-            raise RuntimeError("regrouped plan differs in strata count")
-        self._regroups.append((e, pu, pi))
+    def _build_regroups(self, K: int, B: int, phases, classes: int, waves) -> list:
+        """Regroupings 1..K-1: engines over relabelled ids (user x -> pu[x],
+        item y -> pi[y]) with plans of the same B, classes and phases.  Each
+        shares this engine's persistent-sweep workspace (position counters,
+        error word) when it runs, so failure detection and recovery see its
+        launches too."""
+        out = []
+        for j in range(1, K):
+            rs = np.random.RandomState(self.REGROUP_SEED + j)
+            pu = torch.from_numpy(rs.permutation(self.n_users).astype(np.int64)).to(self.dev)
+            pi = torch.from_numpy(rs.permutation(self.n_items).astype(np.int64)).to(self.dev)
+            uj = pu.index_select(0, self.u.long()).to(torch.int32).cpu().numpy()
+            ij = pi.index_select(0, self.i.long()).to(torch.int32).cpu().numpy()
+            e = SGDEngine(uj, ij, self.r_host, self.n_users, self.n_items, self.k, self.kernel,
+                          self.dtype, self.dev, self.gamma, self.min_rating, self.max_rating,
+                          self.global_mean, eval_order=False)
+            del uj, ij
+            e.strata_persistent = self.strata_persistent
+            e.strata_deep_pipe = self.strata_deep_pipe
+            e.strata_regroup = 1
+            e.prepare_strata(n_blocks=B, waves=waves,
+                             phases=phases if phases is not None and int(phases) > 1 else None,
+                             classes=classes)
+            out.append((e, pu, pi))
+        return out
 
     def _regroup_pick(self, seed: int) -> int:
         """Which plan runs the epoch with rotation seed ``seed`` (0 = this
