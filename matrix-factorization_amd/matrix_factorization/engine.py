@@ -508,7 +508,8 @@ class SGDEngine:
                  n_users: int, n_items: int, n_factors: int, kernel: str,
                  dtype="float64", device=None, gamma: float = 0.0,
                  min_rating: float = 0.0, max_rating: float = 5.0,
-                 global_mean: float = 0.0, eval_order: bool = True):
+                 global_mean: float = 0.0, eval_order: bool = True,
+                 check_ids: bool = True):
         self.dev = resolve_device(device)
         self.dtype = canonical_dtype(dtype)
         self.tdt, self.ndt, self.dcode = DTYPES[self.dtype]
@@ -531,7 +532,7 @@ class SGDEngine:
         self.u_host = np.ascontiguousarray(u, np.int32)
         self.i_host = np.ascontiguousarray(i, np.int32)
         self.r_host = np.ascontiguousarray(r, self.ndt)
-        if self.n and (self.u_host.min() < 0 or self.u_host.max() >= n_users
+        if check_ids and self.n and (self.u_host.min() < 0 or self.u_host.max() >= n_users
                        or self.i_host.min() < 0 or self.i_host.max() >= n_items):
             raise ValueError("rating ids outside [0, n_users) x [0, n_items)")
         self._upload_triples(self.u_host, self.i_host, self.r_host)
@@ -798,7 +799,7 @@ class SGDEngine:
             ij = pi.index_select(0, self.i.long()).to(torch.int32).cpu().numpy()
             e = SGDEngine(uj, ij, self.r_host, self.n_users, self.n_items, self.k, self.kernel,
                           self.dtype, self.dev, self.gamma, self.min_rating, self.max_rating,
-                          self.global_mean, eval_order=False)
+                          self.global_mean, eval_order=False, check_ids=False)
             del uj, ij
             e.strata_persistent = self.strata_persistent
             e.strata_deep_pipe = self.strata_deep_pipe
