@@ -101,7 +101,9 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--variants", nargs="*", default=["C1"],
-                    help="strata plan variants: C<n> = n user-range classes, B<n> = n "
+                    help="strata plan variants (the engine's relabelled plans apply as in the "
+                         "product: 2 with C > 1 and the linear kernel unless "
+                         "MF_STRATA_REGROUP=1): C<n> = n user-range classes, B<n> = n "
                          "blocks, joined with '_' (C2_B128); family strata_<variant> "
                          "(C1: family 'strata')")
     args = ap.parse_args()
