@@ -775,6 +775,8 @@ class SGDEngine:
     REGROUP_SEED = 0x5EED
 
     def _regroup_count(self, classes: int) -> int:
+        if getattr(self, "_regroup_of", None) is not None:
+            return 1                          # a regrouping's own engine: one plan
         k = os.environ.get("MF_STRATA_REGROUP", self.strata_regroup)
         if k in (None, "auto"):
             return (self.REGROUP_AUTO if classes > 1 and self.kernel == "linear"
@@ -804,6 +806,7 @@ class SGDEngine:
             e.strata_persistent = self.strata_persistent
             e.strata_deep_pipe = self.strata_deep_pipe
             e.strata_regroup = 1
+            e._regroup_of = j                 # never regroups itself (env included)
             e.prepare_strata(n_blocks=B, waves=waves,
                              phases=phases if phases is not None and int(phases) > 1 else None,
                              classes=classes)

@@ -556,3 +556,13 @@ def test_regrouped_plans(dtype, phases, K):
     e3 = _engine(u, i, r, nu, ni, k, "linear", dtype, P0, Q0, bu0, bi0)
     e3.prepare_strata(n_blocks=B, classes=1)
     assert len(e3._regroups) == 0
+    # the env override sets the count of the engine's plans, not of its
+    # regroupings' (which never regroup themselves)
+    import os
+    os.environ["MF_STRATA_REGROUP"] = "3"
+    try:
+        e4 = _engine(u, i, r, nu, ni, k, "linear", dtype, P0, Q0, bu0, bi0)
+        e4.prepare_strata(n_blocks=B, classes=C)
+    finally:
+        del os.environ["MF_STRATA_REGROUP"]
+    assert len(e4._regroups) == 2 and all(not e._regroups for e, _, _ in e4._regroups)
