@@ -793,25 +793,32 @@ class SGDEngine:
         error word) when it runs, so failure detection and recovery see its
         launches too."""
         out = []
-        for j in range(1, K):
-            rs = np.random.RandomState(self.REGROUP_SEED + j)
-            pu = torch.from_numpy(rs.permutation(self.n_users).astype(np.int64)).to(self.dev)
-            pi = torch.from_numpy(rs.permutation(self.n_items).astype(np.int64)).to(self.dev)
-            uj = pu.index_select(0, self.u.long()).to(torch.int32).cpu().numpy()
-            ij = pi.index_select(0, self.i.long()).to(torch.int32).cpu().numpy()
-            e = SGDEngine(uj, ij, self.r_host, self.n_users, self.n_items, self.k, self.kernel,
-                          self.dtype, self.dev, self.gamma, self.min_rating, self.max_rating,
-                          self.global_mean, eval_order=False, check_ids=False)
-            del uj, ij
-            e.strata_persistent = self.strata_persistent
-            e.strata_deep_pipe = self.strata_deep_pipe
-            e.strata_regroup = 1
-            e._regroup_of = j                 # never regroups itself (env included)
-            e.prepare_strata(n_blocks=B, waves=waves,
-                             phases=phases if phases is not None and int(phases) > 1 else None,
-                             classes=classes)
-            out.append((e, pu, pi))
+        # (runs on a worker thread: the device is set explicitly, the
+        # thread's current one need not be this engine's)
+        with torch.cuda.device(self.dev):
+            for j in range(1, K):
+                out.append(self._build_regroup(j, B, phases, classes, waves))
         return out
+
+    def _build_regroup(self, j: int, B: int, phases, classes: int, waves):
+        """Regrouping j's engine and its device permutations (pu, pi)."""
+        rs = np.random.RandomState(self.REGROUP_SEED + j)
+        pu = torch.from_numpy(rs.permutation(self.n_users).astype(np.int64)).to(self.dev)
+        pi = torch.from_numpy(rs.permutation(self.n_items).astype(np.int64)).to(self.dev)
+        uj = pu.index_select(0, self.u.long()).to(torch.int32).cpu().numpy()
+        ij = pi.index_select(0, self.i.long()).to(torch.int32).cpu().numpy()
+        e = SGDEngine(uj, ij, self.r_host, self.n_users, self.n_items, self.k, self.kernel,
+                      self.dtype, self.dev, self.gamma, self.min_rating, self.max_rating,
+                      self.global_mean, eval_order=False, check_ids=False)
+        del uj, ij
+        e.strata_persistent = self.strata_persistent
+        e.strata_deep_pipe = self.strata_deep_pipe
+        e.strata_regroup = 1
+        e._regroup_of = j                 # never regroups itself (env included)
+        e.prepare_strata(n_blocks=B, waves=waves,
+                         phases=phases if phases is not None and int(phases) > 1 else None,
+                         classes=classes)
+        return e, pu, pi
 
     def _regroup_pick(self, seed: int) -> int:
         """Which plan runs the epoch with rotation seed ``seed`` (0 = this
