@@ -602,7 +602,8 @@ struct StrataSeq { uint16_t s[kStrataSeqArg]; };
 // checks occupancy, then launches cooperatively (hipLaunchCooperativeKernel:
 // the runtime refuses a grid that cannot be resident at once, and the epoch
 // then runs as one launch per stratum).
-template <typename T, int W, int GS, int V, int KERN, int S, int DEPTH = 1, int NW = kStrataWaves>
+template <typename T, int W, int GS, int V, int KERN, int S, int DEPTH = 1, int NW = kStrataWaves,
+          bool CLS = false>
 __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A,
                                                                     const StrataSeq seq,
                                                                     int32_t n_seq, int32_t* done,
@@ -692,40 +693,25 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
         if (s_l2ok < 0) return;           // the launch failed: nothing applied here
         l2ok = s_l2ok != 0;
     }
-    const int C = A.cls;
-    // Early poll (C > 1): the next position's user range was released C - 1
-    // blocks before it is needed, so its holder's counter is read ONCE,
-    // during the current block (issued after the block's prologue, read at
-    // its end); when that shows the range released, the next position starts
-    // without the poll's round trip and its barrier.  The next position's
-    // geometry (scalar loads) is read beside the current block's drain.
-    const __amdgpu_buffer_rsrc_t drs = buf_rsrc(done, (uint64_t)B * sizeof(int32_t));
-    // position geometry: stratum, user range, and the workgroup that held the
-    // range C positions back (scalar loads; each position's are issued two
-    // positions ahead, inside a block, so no wait at a block boundary meets
-    // them)
-    struct Geo { int s, ulo, nus, wd; };
-    auto geo = [&](int t) __attribute__((always_inline)) {
-        Geo g;
-        g.s = seq.s[t];
-        const int ub = (g.s + C * w) % (C * B);
-        g.ulo = A.ubnd[ub];
-        g.nus = A.ubnd[ub + 1] - g.ulo;
-        g.wd = t >= C ? (w + g.s / C - (int)seq.s[t - C] / C + 2 * B) % B : 0;
-        return g;
-    };
-    Geo gc = geo(0);
-    Geo gn = n_seq > 1 ? geo(1) : gc;
-    bool ready = false;                  // position t's range seen released (uniform)
-    for (int t = 0; t < n_seq; ++t) {
-        stamp(t, 0);
-        if (!ready) {
+    if constexpr (!CLS) {
+        // one class: the next position's holder is the previous position's
+        // workgroup, finishing right now -- nothing to poll early or publish
+        // late; the geometry is read at the top of each position, where the
+        // poll's round trip hides it (the multi-class loop below, run with
+        // one class, was 1-7 % slower: same-box A/B r04y / r04z)
+        const int C = A.cls;
+        for (int t = 0; t < n_seq; ++t) {
+            const int s = seq.s[t];
+            const int ub = (s + C * w) % (C * B);
+            const int ulo = A.ubnd[ub], nus = A.ubnd[ub + 1] - ulo;
+            stamp(t, 0);
             if (threadIdx.x == 0) {
                 int ab = 0;
                 if (t >= C) {
                     // the user range's previous holder: same class, C positions back
+                    const int wd = (w + s / C - (int)seq.s[t - C] / C + 2 * B) % B;
                     int64_t spins = 0;
-                    while (__hip_atomic_load(done + gc.wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                    while (__hip_atomic_load(done + wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
                            base + t - C + 1) {
                         __builtin_amdgcn_s_sleep(2);
                         if (++spins > kStrataSpinLimit ||
@@ -743,63 +729,144 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
             }
             __syncthreads();
             if (s_abort) return;
-        }
-        stamp(t, 1);
-        const bool more = t + 1 < n_seq;
-        // the early poll: one sc1 buffer load of the next range's holder's
-        // counter, every lane the same word, dropped (no access) when unused
-        const bool ep = A.early && more && C > 1 && t + 1 >= C;
-        int poll = 0;
-        Geo g2 = gn;
-        auto hook = [&]() __attribute__((always_inline)) {
-            poll = buf_ld<16, int>(drs, ep ? (uint32_t)gn.wd * (uint32_t)sizeof(int32_t) : kBufDrop);
-            if (t + 2 < n_seq) g2 = geo(t + 2);
-        };
-        // the user-bias slice is staged inside the block, behind its prologue
-        // the next holder of this user range, w + s_t - s_{t+1}, on this XCD
-        // (same residue mod 8, B a multiple of 8): rows stored plainly stay
-        // in the L2 it reads; otherwise write-through, as always
-        const bool keep = l2ok && more && ((gc.s - gn.s) & 7) == 0;
-        strata_block<T, W, GS, V, KERN, S, true, true, DEPTH, NW>(A, (int64_t)gc.s * B + w, gc.ulo, ilo,
-                                                              Qs, Bis, Bus, h, gc.nus, keep, hook);
-        // lane 0 decides for the workgroup (the barrier below publishes it);
-        // every wave's loads of the next range come after that barrier
-        if (threadIdx.x == 0)
-            s_next = A.early && more && C > 1 && (t + 1 < C || poll >= base + t + 2 - C);
-        __syncthreads();
-        stamp(t, 2);
-        const bool rdy = s_next != 0;
-        if constexpr (KERN != MF_RBF) {
-            if (A.upd_user)
-                for (int x = threadIdx.x; x < gc.nus; x += TH)
-                    __hip_atomic_store(A.Bu + gc.ulo + x, Bus[x], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);     // write-through
-        }
-        // every storing wave drains its write-through stores, then one lane
-        // signals (no L2 write-back fence: nothing handed off sits dirty in L2).
-        // With C > 1 a range's next holder comes C positions later, so the
-        // drain and the signal are taken every D = C - 1 positions (and at the
-        // last): the counter then jumps by D, each range is published at most
-        // D - 1 blocks late, i.e. still before its next holder's position --
-        // D - 1 of every D drains off the chain.  In between, a barrier only
-        // (the next block rewrites the bias slice the stores above read).
-        const int D = C > 1 ? C - 1 : 1;
-        if (!more || t % D == D - 1) {
+            stamp(t, 1);
+            // the user-bias slice is staged inside the block, behind its prologue
+            // the next holder of this user range, w + s_t - s_{t+1}, on this XCD
+            // (same residue mod 8, B a multiple of 8): rows stored plainly stay
+            // in the L2 it reads; otherwise write-through, as always
+            const bool keep = l2ok && t + 1 < n_seq && ((s - (int)seq.s[t + 1]) & 7) == 0;
+            strata_block<T, W, GS, V, KERN, S, true, true, DEPTH, NW>(A, (int64_t)s * B + w, ulo, ilo, Qs,
+                                                                  Bis, Bus, h, nus, keep);
+            __syncthreads();
+            stamp(t, 2);
+            if constexpr (KERN != MF_RBF) {
+                if (A.upd_user)
+                    for (int x = threadIdx.x; x < nus; x += TH)
+                        __hip_atomic_store(A.Bu + ulo + x, Bus[x], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);     // write-through
+            }
+            // every storing wave drains its write-through stores, then one lane
+            // signals (no L2 write-back fence: nothing handed off sits dirty in L2)
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             if (threadIdx.x == 0) {
                 // L2 hand-offs: rows of this range stored plainly by earlier blocks
                 // on this XCD must reach memory before another XCD reads them
-                if (l2ok && !keep && more) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                if (l2ok && !keep && t + 1 < n_seq) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
                 __hip_atomic_store(done + w, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
-        } else {
-            __syncthreads();
+            stamp(t, 3);
         }
-        stamp(t, 3);
-        ready = rdy;
-        gc = gn;
-        gn = g2;
+    } else {
+        const int C = A.cls;
+        // Early poll (C > 1): the next position's user range was released C - 1
+        // blocks before it is needed, so its holder's counter is read ONCE,
+        // during the current block (issued after the block's prologue, read at
+        // its end); when that shows the range released, the next position starts
+        // without the poll's round trip and its barrier.  The next position's
+        // geometry (scalar loads) is read beside the current block's drain.
+        const __amdgpu_buffer_rsrc_t drs = buf_rsrc(done, (uint64_t)B * sizeof(int32_t));
+        // position geometry: stratum, user range, and the workgroup that held the
+        // range C positions back (scalar loads; each position's are issued two
+        // positions ahead, inside a block, so no wait at a block boundary meets
+        // them)
+        struct Geo { int s, ulo, nus, wd; };
+        auto geo = [&](int t) __attribute__((always_inline)) {
+            Geo g;
+            g.s = seq.s[t];
+            const int ub = (g.s + C * w) % (C * B);
+            g.ulo = A.ubnd[ub];
+            g.nus = A.ubnd[ub + 1] - g.ulo;
+            g.wd = t >= C ? (w + g.s / C - (int)seq.s[t - C] / C + 2 * B) % B : 0;
+            return g;
+        };
+        Geo gc = geo(0);
+        Geo gn = n_seq > 1 ? geo(1) : gc;
+        bool ready = false;                  // position t's range seen released (uniform)
+        for (int t = 0; t < n_seq; ++t) {
+            stamp(t, 0);
+            if (!ready) {
+                if (threadIdx.x == 0) {
+                    int ab = 0;
+                    if (t >= C) {
+                        // the user range's previous holder: same class, C positions back
+                        int64_t spins = 0;
+                        while (__hip_atomic_load(done + gc.wd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                               base + t - C + 1) {
+                            __builtin_amdgcn_s_sleep(2);
+                            if (++spins > kStrataSpinLimit ||
+                                __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                ab = 1;
+                                break;
+                            }
+                        }
+                        // every load of handed-off bytes below is sc1: no L1 invalidate,
+                        // only keep the compiler from hoisting them above the poll
+                        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    }
+                    s_abort = ab;
+                }
+                __syncthreads();
+                if (s_abort) return;
+            }
+            stamp(t, 1);
+            const bool more = t + 1 < n_seq;
+            // the early poll: one sc1 buffer load of the next range's holder's
+            // counter, every lane the same word, dropped (no access) when unused
+            const bool ep = A.early && more && C > 1 && t + 1 >= C;
+            int poll = 0;
+            Geo g2 = gn;
+            auto hook = [&]() __attribute__((always_inline)) {
+                poll = buf_ld<16, int>(drs, ep ? (uint32_t)gn.wd * (uint32_t)sizeof(int32_t) : kBufDrop);
+                if (t + 2 < n_seq) g2 = geo(t + 2);
+            };
+            // the user-bias slice is staged inside the block, behind its prologue
+            // the next holder of this user range, w + s_t - s_{t+1}, on this XCD
+            // (same residue mod 8, B a multiple of 8): rows stored plainly stay
+            // in the L2 it reads; otherwise write-through, as always
+            const bool keep = false;             // (the L2 hand-off needs one class)
+            strata_block<T, W, GS, V, KERN, S, true, true, DEPTH, NW>(A, (int64_t)gc.s * B + w, gc.ulo, ilo,
+                                                                  Qs, Bis, Bus, h, gc.nus, keep, hook);
+            // lane 0 decides for the workgroup (the barrier below publishes it);
+            // every wave's loads of the next range come after that barrier
+            if (threadIdx.x == 0)
+                s_next = A.early && more && C > 1 && (t + 1 < C || poll >= base + t + 2 - C);
+            __syncthreads();
+            stamp(t, 2);
+            const bool rdy = s_next != 0;
+            if constexpr (KERN != MF_RBF) {
+                if (A.upd_user)
+                    for (int x = threadIdx.x; x < gc.nus; x += TH)
+                        __hip_atomic_store(A.Bu + gc.ulo + x, Bus[x], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);     // write-through
+            }
+            // every storing wave drains its write-through stores, then one lane
+            // signals (no L2 write-back fence: nothing handed off sits dirty in L2).
+            // With C > 1 a range's next holder comes C positions later, so the
+            // drain and the signal are taken every D = C - 1 positions (and at the
+            // last): the counter then jumps by D, each range is published at most
+            // D - 1 blocks late, i.e. still before its next holder's position --
+            // D - 1 of every D drains off the chain.  In between, a barrier only
+            // (the next block rewrites the bias slice the stores above read).
+            const int D = C > 1 ? C - 1 : 1;
+            if (!more || t % D == D - 1) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    // L2 hand-offs: rows of this range stored plainly by earlier blocks
+                    // on this XCD must reach memory before another XCD reads them
+                    if (l2ok && !keep && more) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                    __hip_atomic_store(done + w, base + t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            } else {
+                __syncthreads();
+            }
+            stamp(t, 3);
+            ready = rdy;
+            gc = gn;
+            gn = g2;
+        }
     }
     __syncthreads();
     if (A.Dq)
@@ -1019,9 +1086,14 @@ struct StrataRun {
             strata_class_cycle(p.seq, p.n_seq, a.cls)) {
             // (the deep pipeline exists for the 16- and 8-wave kernels)
             constexpr int kDeep = NW >= 8 ? 2 : 1;
-            auto efn = (kDeep == 2 && (p.flags & MF_FLAG_DEEP_PIPE))
-                           ? k_sgd_strata_epoch<T, W, GS, V, KERN, S, kDeep, NW>
-                           : k_sgd_strata_epoch<T, W, GS, V, KERN, S, 1, NW>;
+            // (user-range classes C > 1: the loop that polls the next range
+            // during the current block and publishes every C - 1 positions)
+            const bool deep = kDeep == 2 && (p.flags & MF_FLAG_DEEP_PIPE);
+            auto efn = a.cls > 1
+                           ? (deep ? k_sgd_strata_epoch<T, W, GS, V, KERN, S, kDeep, NW, true>
+                                   : k_sgd_strata_epoch<T, W, GS, V, KERN, S, 1, NW, true>)
+                           : (deep ? k_sgd_strata_epoch<T, W, GS, V, KERN, S, kDeep, NW, false>
+                                   : k_sgd_strata_epoch<T, W, GS, V, KERN, S, 1, NW, false>);
             MF_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(efn),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
             persistent = strata_coresident(reinterpret_cast<const void*>(efn), p.B, lds, TH);
