@@ -509,7 +509,7 @@ class SGDEngine:
                  dtype="float64", device=None, gamma: float = 0.0,
                  min_rating: float = 0.0, max_rating: float = 5.0,
                  global_mean: float = 0.0, eval_order: bool = True,
-                 check_ids: bool = True):
+                 check_ids: bool = True, device_triples=None):
         self.dev = resolve_device(device)
         self.dtype = canonical_dtype(dtype)
         self.tdt, self.ndt, self.dcode = DTYPES[self.dtype]
@@ -535,7 +535,10 @@ class SGDEngine:
         if check_ids and self.n and (self.u_host.min() < 0 or self.u_host.max() >= n_users
                        or self.i_host.min() < 0 or self.i_host.max() >= n_items):
             raise ValueError("rating ids outside [0, n_users) x [0, n_items)")
-        self._upload_triples(self.u_host, self.i_host, self.r_host)
+        if device_triples is not None:       # (u, i, r) already on the device
+            self.u, self.i, self.r = device_triples
+        else:
+            self._upload_triples(self.u_host, self.i_host, self.r_host)
         if eval_order:
             self._build_eval()
         else:                        # a regrouping's engine: sweeps only, no RMSE pass
@@ -805,12 +808,15 @@ class SGDEngine:
         rs = np.random.RandomState(self.REGROUP_SEED + j)
         pu = torch.from_numpy(rs.permutation(self.n_users).astype(np.int64)).to(self.dev)
         pi = torch.from_numpy(rs.permutation(self.n_items).astype(np.int64)).to(self.dev)
-        uj = pu.index_select(0, self.u.long()).to(torch.int32).cpu().numpy()
-        ij = pi.index_select(0, self.i.long()).to(torch.int32).cpu().numpy()
-        e = SGDEngine(uj, ij, self.r_host, self.n_users, self.n_items, self.k, self.kernel,
-                      self.dtype, self.dev, self.gamma, self.min_rating, self.max_rating,
-                      self.global_mean, eval_order=False, check_ids=False)
-        del uj, ij
+        uj_d = pu.index_select(0, self.u.long()).to(torch.int32)
+        ij_d = pi.index_select(0, self.i.long()).to(torch.int32)
+        # the relabelled ids stay on the device for the engine (no re-upload),
+        # the ratings are this engine's (read-only); the host copies feed the
+        # planner
+        e = SGDEngine(uj_d.cpu().numpy(), ij_d.cpu().numpy(), self.r_host, self.n_users,
+                      self.n_items, self.k, self.kernel, self.dtype, self.dev, self.gamma,
+                      self.min_rating, self.max_rating, self.global_mean, eval_order=False,
+                      check_ids=False, device_triples=(uj_d, ij_d, self.r))
         e.strata_persistent = self.strata_persistent
         e.strata_deep_pipe = self.strata_deep_pipe
         e.strata_regroup = 1
