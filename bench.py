@@ -107,16 +107,20 @@ def synth(n_users: int, n_items: int, nnz: int, seed: int = 20261015):
 
 
 def traffic_from_profiles(workload: str, n_gpus: int, schedule: str, dtype: str,
-                          kernel: str):
+                          kernel: str, emulate: int = 0):
     """HBM bytes per SGD launch measured by rocprofv3 PMC passes for exactly
-    this workload, schedule, dtype and kernel, if committed under
+    this workload, schedule, dtype, kernel and world size, if committed under
     profiles/traffic.json; else None (the line then says `traffic: null`
-    rather than borrowing another configuration's counters)."""
+    rather than borrowing another configuration's counters).  ``emulate``
+    (one GPU running rank 0 of an N-rank rotation, --emulate-rank N): the
+    key is ``emu{N}``, never the N = 1 run's ``n1`` -- the emulated sub-epochs
+    are other launches on other plans."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        e = d.get(f"{workload}/{schedule}/{dtype}/n{n_gpus}")
+        world = f"emu{emulate}" if emulate > 1 else f"n{n_gpus}"
+        e = d.get(f"{workload}/{schedule}/{dtype}/{world}")
         if e is None or e.get("kernel") != kernel:
             return None
         return float(e["hbm_bytes_per_sgd_launch"])
@@ -883,7 +887,10 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
     rotate = (world > 1 or emu > 1) and strata and args.exchange == "rotate"
     ilo = item_ranges(i, ni, max(world, emu)) if rotate else None
     if strata:
-        plan = eng.prepare_strata(n_blocks=args.blocks, waves=args.waves, item_bounds=ilo)
+        # (the delta exchange's epochs always run the engine's own plan: no
+        # relabelled plans for it)
+        plan = eng.prepare_strata(n_blocks=args.blocks, waves=args.waves, item_bounds=ilo,
+                                  regroup=1 if (world > 1 and not rotate) else None)
         nb = plan.n_strata                   # strata per epoch (C*B with C user-range classes)
         B = plan.B                           # workgroups / item slabs
         cls = plan.classes
@@ -1117,7 +1124,7 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
                      else "k_sgd_batch")
             traffic = traffic_from_profiles(args.workload, world, args.schedule
                                             + ("_persistent" if persistent else ""),
-                                            args.dtype, kname)
+                                            args.dtype, kname, emulate=emu)
             roofline = {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -8,6 +8,8 @@
 #include <cstdlib>
 #include <functional>
 #include <memory>
+#include <exception>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -24,19 +26,46 @@ inline int host_threads() {
     return (int)std::max(1u, std::min(16u, hw));
 }
 
+// The first exception thrown on any worker thread (bad_alloc of a scratch
+// vector, ...), rethrown on the calling thread after every worker joined --
+// an exception escaping a std::thread would call std::terminate instead of
+// reaching the C ABI's error path.
+struct ThreadErr {
+    std::mutex m;
+    std::exception_ptr e;
+    template <class F>
+    void guard(F&& f) {
+        try {
+            f();
+        } catch (...) {
+            std::lock_guard<std::mutex> g(m);
+            if (!e) e = std::current_exception();
+        }
+    }
+    bool failed() {
+        std::lock_guard<std::mutex> g(m);
+        return (bool)e;
+    }
+    void rethrow() {
+        if (e) std::rethrow_exception(e);
+    }
+};
+
 // fn(t, lo, hi) over [0, n) cut into T contiguous chunks
 inline void parallel_chunks(int64_t n, int T, const std::function<void(int, int64_t, int64_t)>& fn) {
     if (T <= 1 || n < (int64_t)1 << 16) {
         fn(0, 0, n);
         return;
     }
+    ThreadErr err;
     std::vector<std::thread> th;
     th.reserve(T);
     for (int t = 0; t < T; ++t) {
         const int64_t lo = n * t / T, hi = n * (t + 1) / T;
-        th.emplace_back(fn, t, lo, hi);
+        th.emplace_back([&, t, lo, hi]() { err.guard([&]() { fn(t, lo, hi); }); });
     }
     for (auto& x : th) x.join();
+    err.rethrow();
 }
 
 // Large host scratch buffers (10^8 entries at C3): anonymous mappings with
@@ -111,15 +140,19 @@ void partition_rows(int64_t n, int NB, int T, F bucket, std::vector<int64_t>& st
 template <class F>
 void for_buckets(int NB, int T, F fn, const std::atomic<int>* stop = nullptr) {
     std::atomic<int> next{0};
+    ThreadErr err;
     auto work = [&]() {
-        for (int b; !(stop && stop->load(std::memory_order_relaxed)) &&
-                    (b = next.fetch_add(1)) < NB;)
-            fn(b);
+        err.guard([&]() {
+            for (int b; !(stop && stop->load(std::memory_order_relaxed)) &&
+                        (b = next.fetch_add(1)) < NB;)
+                fn(b);
+        });
     };
     std::vector<std::thread> th;
     for (int t = 1; t < std::min(T, NB); ++t) th.emplace_back(work);
     work();
     for (auto& x : th) x.join();
+    err.rethrow();
 }
 
 }  // namespace mf

@@ -99,7 +99,10 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, const int32_t* brow, in
     // (the order a (load, slot) min-heap pops): one bit set of slots per load
     // level, the lowest set bit of the lowest non-empty level is the slot
     const int32_t WD = (NS + 63) / 64;
-    int32_t cap = maxdeg * (int32_t)S.order.size() / NS + maxdeg + 2;   // > any load reached
+    // > any load reached: LPT puts a user on a slot loaded <= m / NS (the
+    // mean), so no load exceeds m / NS + maxdeg (int64: no overflow for a
+    // block of a heavy user among many)
+    int64_t cap = (int64_t)m / NS + maxdeg + 2;
     S.lvl.assign((size_t)cap * WD, 0);
     for (int32_t x = 0; x < NS; ++x) S.lvl[(size_t)(x >> 6)] |= 1ull << (x & 63);
     S.load.assign(NS, 0);
@@ -118,9 +121,9 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, const int32_t* brow, in
         }
         S.lvl[(size_t)low * WD + (slot >> 6)] &= ~(1ull << (slot & 63));
         const int32_t nl = low + S.ucnt[ul];
-        if (nl >= cap) {                                          // grow (never at C3)
+        if (nl >= cap) {                                          // grow (never reached)
             S.lvl.resize((size_t)(nl + 1) * WD, 0);
-            cap = nl + 1;
+            cap = (int64_t)nl + 1;
         }
         S.lvl[(size_t)nl * WD + (slot >> 6)] |= 1ull << (slot & 63);
         S.uslot[ul] = slot;
@@ -383,9 +386,11 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
     const unsigned nt = (unsigned)std::min<int64_t>(hw, std::max<int64_t>(1, n / 200000));
     auto blocks = [&](bool colour, const int64_t* bstep, int32_t* sched) {
         std::atomic<int64_t> next{0};
-        auto worker = [&]() {
+        mf::ThreadErr err;
+        auto worker = [&]() { err.guard([&]() {
             Scratch S;
             for (;;) {
+                if (err.failed()) break;               // another worker threw: stop
                 const int64_t c = next.fetch_add(1);
                 if (c >= nch) break;
                 for (int64_t b = c * CH; b < std::min(BB, (c + 1) * CH); ++b) {
@@ -400,11 +405,12 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
                     if (!colour) steps[b] = d;
                 }
             }
-        };
+        }); };
         std::vector<std::thread> th;
         for (unsigned t = 1; t < nt; ++t) th.emplace_back(worker);
         worker();
         for (auto& t : th) t.join();
+        err.rethrow();                                 // -> the C ABI's bad_alloc path
     };
     blocks(false, nullptr, nullptr);
     lap("block steps");
@@ -456,6 +462,10 @@ extern "C" int mf_strata_plan_build_classes(const int32_t* user_ids, const int32
         if (plan_out) *plan_out = nullptr;
         set_error("out of host memory (strata plan of %lld ratings)", (long long)n);
         return MF_ERR_NOMEM;
+    } catch (const std::exception& e) {
+        if (plan_out) *plan_out = nullptr;
+        set_error("strata planner failed: %s", e.what());
+        return MF_ERR_INVALID;
     }
 }
 

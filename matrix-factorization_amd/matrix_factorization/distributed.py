@@ -676,7 +676,10 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
         ex = ReplicaExchange(eng, group)
         ex.bind(Q0, bi0)
         if strata:
-            eng.prepare_strata()
+            # delta-out epochs always run the engine's own plan: no
+            # relabelled plans unless items are frozen (update_users runs
+            # plain epochs, which do pick them)
+            eng.prepare_strata(regroup=None if not update_item else 1)
             nb = eng.strata
         else:
             eng.prepare_colored()

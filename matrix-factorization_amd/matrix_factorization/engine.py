@@ -669,7 +669,8 @@ class SGDEngine:
                        waves: Optional[int] = None,
                        phases: Optional[int] = None,
                        item_bounds: Optional[np.ndarray] = None,
-                       classes: Optional[int] = None) -> "StrataPlan":
+                       classes: Optional[int] = None,
+                       regroup: Optional[int] = None) -> "StrataPlan":
         """Build the stratified plan once and store a padded copy of the
         ratings in plan order (block-major, step-major, slot-minor).  The
         host arrays keep the original rating order.
@@ -695,7 +696,13 @@ class SGDEngine:
         blocks of slack, and an item meets 1/C of a block's ratings per user
         range).  None = ``strata_classes`` / env MF_STRATA_CLASSES; "auto"
         (the default) = ``auto_classes`` for the engine's own B (n_blocks
-        None, no item_bounds), else 1."""
+        None, no item_bounds), else 1.
+
+        ``regroup``: relabelled plans to build (1 = none); None = by
+        ``strata_regroup`` / env MF_STRATA_REGROUP.  Engines that only run
+        the delta-out form (exchange="delta") pass 1: delta epochs always
+        run the engine's own plan, so regroupings would be dead weight (a
+        second padded copy of the ratings and of P / Q)."""
         if self.colored is not None or self.strata is not None:
             raise RuntimeError("ratings already permuted by another schedule")
         classes = self._classes(classes)
@@ -731,7 +738,9 @@ class SGDEngine:
         # the regroupings' plans (same B, classes and phases) are built on a
         # worker thread while this one builds the engine's own: the planner
         # is host code that releases the GIL
-        K = self._regroup_count(classes)
+        K = self._regroup_count(classes) if regroup is None else int(regroup)
+        if not 1 <= K <= self.REGROUP_MAX:
+            raise ValueError(f"strata regroupings must be in [1, {self.REGROUP_MAX}], got {K}")
         worker = None
         if K > 1 and n_blocks is not None:
             worker = ThreadPoolExecutor(1)
@@ -834,11 +843,13 @@ class SGDEngine:
             return 0
         return int((((int(seed) & 0xFFFFFFFF) * 2654435761) & 0xFFFFFFFF) >> 16) % K
 
-    def serial_order(self, seq, seed) -> np.ndarray:
+    def serial_order(self, seq, seed, delta: bool = False) -> np.ndarray:
         """The rating indices in the order the strata epoch (seq, seed)
         applies them, whichever plan it picks (indices into this engine's
-        rating arrays; a regrouping lists the same ratings)."""
-        j = self._regroup_pick(seed)
+        rating arrays; a regrouping lists the same ratings).  ``delta``: the
+        epoch ran in delta-out form, which always runs the engine's own plan
+        (epoch_strata with ``delta``)."""
+        j = 0 if delta else self._regroup_pick(seed)
         pl = self.strata if j == 0 else self._regroups[j - 1][0].strata
         return pl.serial_order(seq, seed)
 
@@ -1628,9 +1639,13 @@ class _ErrorPoll:
         if ws is None or self.ev is not None and not self.ev.query():
             return                                # the last copy is still in flight
         B = self.e.strata.B
-        self.host.copy_(ws[B:B + 1], non_blocking=True)
-        self.ev = torch.cuda.Event()
-        self.ev.record()
+        # the copy and its event on the ENGINE's stream (its device's current
+        # stream), not the current device's: the engine may live on another
+        # device than the caller's current one
+        with torch.cuda.device(self.e.dev):
+            self.host.copy_(ws[B:B + 1], non_blocking=True)
+            self.ev = torch.cuda.Event()
+            self.ev.record(torch.cuda.current_stream(self.e.dev))
 
     def failed(self) -> bool:
         return self.ev is not None and self.ev.query() and int(self.host[0]) != 0

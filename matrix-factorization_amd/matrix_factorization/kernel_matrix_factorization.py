@@ -42,6 +42,7 @@ Three keyword arguments are new and default to the reference's behaviour:
 
 from __future__ import annotations
 
+import contextlib
 from concurrent.futures import ThreadPoolExecutor
 from typing import Union
 
@@ -50,7 +51,7 @@ import pandas as pd
 
 from . import _lib
 from .distributed import EXCHANGES, fit_sharded, world_info
-from .engine import SGDEngine, canonical_dtype, fit_epochs
+from .engine import SGDEngine, canonical_dtype, fit_epochs, resolve_device
 from .recommender_base import RecommenderBase
 
 
@@ -136,24 +137,39 @@ class KernelMF(RecommenderBase):
 
     # ----------------------------------------------------- device state
     def _make_engine(self, X: pd.DataFrame, n_users: int, n_items: int,
-                     schedule: str = None) -> SGDEngine:
+                     schedule: str = None, device=None, worker: bool = False) -> SGDEngine:
         """Ratings uploaded, evaluation order built and, for ``schedule``
         "strata" / "colored", the schedule planned (what fit_epochs would
-        otherwise do first)."""
+        otherwise do first).
+
+        ``device``: the concrete device, resolved by the CALLER (the current
+        device is thread-local: a worker thread would see device 0 whatever
+        the caller's ``torch.cuda.set_device``).  ``worker``: built on a
+        worker thread -- its copies ran on that thread's current stream of
+        ``device``, which is synchronised before the engine is handed back,
+        so the caller's stream (e.g. inside ``with torch.cuda.stream(s)``)
+        never races them."""
+        import torch
+
+        dev = resolve_device(self.device) if device is None else device
         n = len(X)
         u = X["user_id"].to_numpy(np.int32) if n else np.zeros(0, np.int32)
         i = X["item_id"].to_numpy(np.int32) if n else np.zeros(0, np.int32)
         r = X["rating"].to_numpy(np.float64) if n else np.zeros(0)
-        eng = SGDEngine(u, i, r, n_users, n_items,
-                        self.n_factors, self.kernel, self.dtype, self.device,
-                        gamma=self.gamma, min_rating=self.min_rating,
-                        max_rating=self.max_rating, global_mean=self.global_mean)
-        eng.strata_classes = getattr(self, "strata_classes", "auto")
-        eng.strata_regroup = getattr(self, "strata_regroup", "auto")
-        if schedule == "strata" and n:
-            eng.prepare_strata()
-        elif schedule == "colored" and n:
-            eng.prepare_colored()
+        on_gpu = isinstance(dev, torch.device) and dev.type == "cuda"
+        with (torch.cuda.device(dev) if on_gpu else contextlib.nullcontext()):
+            eng = SGDEngine(u, i, r, n_users, n_items,
+                            self.n_factors, self.kernel, self.dtype, dev,
+                            gamma=self.gamma, min_rating=self.min_rating,
+                            max_rating=self.max_rating, global_mean=self.global_mean)
+            eng.strata_classes = getattr(self, "strata_classes", "auto")
+            eng.strata_regroup = getattr(self, "strata_regroup", "auto")
+            if schedule == "strata" and n:
+                eng.prepare_strata()
+            elif schedule == "colored" and n:
+                eng.prepare_colored()
+            if worker and on_gpu:
+                torch.cuda.current_stream(dev).synchronize()
         return eng
 
     def _sync_params(self, eng: SGDEngine) -> None:
@@ -238,7 +254,7 @@ class KernelMF(RecommenderBase):
                 # initial factors: the worker draws nothing, so the RNG
                 # stream is the reference's (sample, normal P, normal Q)
                 fut = ex.submit(self._make_engine, X, self.n_users, self.n_items,
-                                self.schedule)
+                                self.schedule, resolve_device(self.device), True)
             self.user_features = np.random.normal(self.init_mean, self.init_sd,
                                                   (self.n_users, self.n_factors))
             self.item_features = np.random.normal(self.init_mean, self.init_sd,

@@ -79,7 +79,7 @@ class CpuEngine:
         self.colored = offs
         return len(offs) - 1
 
-    def prepare_strata(self, n_blocks=None, item_bounds=None, classes=None):
+    def prepare_strata(self, n_blocks=None, item_bounds=None, classes=None, regroup=None):
         from matrix_factorization.engine import (PhasedStrata, StrataPlan, balanced_bounds,
                                                  sched_strata, strata_slots)
 

@@ -227,6 +227,7 @@ def cpu_engine(monkeypatch):
     import matrix_factorization.kernel_matrix_factorization as kmf
 
     monkeypatch.setattr(kmf, "SGDEngine", OracleEngine)
+    monkeypatch.setattr(kmf, "resolve_device", lambda device=None: device)
     monkeypatch.setattr(bm, "SGDEngine", OracleEngine)
     return OracleEngine
 
@@ -559,3 +560,23 @@ def test_deep_pipe_default_by_plan_shape(monkeypatch):
     assert deep(plan(ns8, 1050)) is False
     monkeypatch.setenv("MF_STRATA_DEEP", "1")
     assert deep(plan(ns16, 1100)) is True
+
+
+def test_bench_traffic_lookup_is_keyed_on_world_and_emulation():
+    """bench.py's roofline.traffic comes from PMC counters of exactly the
+    configuration measured: an --emulate-rank N line must not borrow the
+    N = 1 run's counters."""
+    import sys
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    got = bench.traffic_from_profiles("c3", 1, "strata_persistent", "float32",
+                                      "k_sgd_strata_epoch")
+    assert got is not None and got > 1e9                      # the committed N = 1 counters
+    assert bench.traffic_from_profiles("c3", 1, "strata_persistent", "float32",
+                                       "k_sgd_strata_epoch", emulate=8) is None
+    assert bench.traffic_from_profiles("c3", 8, "strata_persistent", "float32",
+                                       "k_sgd_strata_epoch") is None
+    assert bench.traffic_from_profiles("c3", 1, "strata_persistent", "float32",
+                                       "k_sgd_strata") is None     # another kernel

@@ -14,6 +14,7 @@
 #   trace[:ARGS]         rocprofv3 --kernel-trace --stats -- python bench.py ARGS
 #   pmc:CTRS[:ARGS]      rocprofv3 --pmc CTRS (+ kernel trace) -- python bench.py ARGS
 #                        (CTRS '+'-separated; one pass, within the per-block limits)
+#   pmcpy:CTRS:SCRIPT[:ARGS]  rocprofv3 --pmc CTRS -- python SCRIPT ARGS (one pass)
 #   calib                FETCH_SIZE / WRITE_SIZE passes over tools/calib_fetch
 #   py:SCRIPT[:ARGS]     python SCRIPT ARGS              (probes under tools/; limit
 #                        $PY_TIMEOUT s, default 600 -- set it with env:PY_TIMEOUT=N)
@@ -54,6 +55,15 @@ for step in "$@"; do
         [[ "$rest" == *:* ]] && bargs=${rest#*:}
         timeout -s KILL 300 rocprofv3 --pmc ${ctrs//+/ } --kernel-trace --output-format csv -d "$p" \
             -o run -- python "$R/bench.py" ${bargs//,/ } > "$p.json" 2> "$p.log" ;;
+    pmcpy)
+        # pmcpy:CTRS:SCRIPT[:ARGS] -- one PMC pass over a probe script
+        ctrs=${rest%%:*}
+        srest=${rest#*:}
+        script=${srest%%:*}
+        sargs=""
+        [[ "$srest" == *:* ]] && sargs=${srest#*:}
+        timeout -s KILL 300 rocprofv3 --pmc ${ctrs//+/ } --kernel-trace --output-format csv -d "$p" \
+            -o run -- python "$R/$script" ${sargs//,/ } > "$p.out" 2> "$p.log" ;;
     calib)
         timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv \
             -d "${p}_fetch" -o run -- "$R/tools/calib_fetch" > "${p}_fetch.log" 2>&1
