@@ -84,6 +84,13 @@ enum {
                                  for each position's user range at its start
                                  instead of polling it once during the previous
                                  block (diagnostic A/B) */
+    MF_FLAG_STREAM = 1024,    /* with MF_FLAG_PERSISTENT, MF_FLAG_DEEP_PIPE and
+                                 classes C > 1: the stream form -- one software
+                                 pipeline through all positions of the launch
+                                 (the next block's triples and user rows loaded
+                                 while the current block's last steps apply,
+                                 the bias slices double-buffered in LDS); the
+                                 same sequential order, bit for bit */
     /* mf_sgd_epoch_strata: bits 24..27 = C - 1, the plan's user-range classes
        (mf_strata_plan_build_classes; 0 = C = 1, the plain B x B plan) */
     MF_FLAG_CLASSES_SHIFT = 24
@@ -499,6 +506,26 @@ int mf_sched_levels(const int32_t* user_ids, const int32_t* item_ids,
                     int64_t offsets_cap, int32_t* n_levels_out);
 
 /*
+ * The exact-order schedule at scale (replaces the per-epoch host cost of
+ * `np.random.shuffle(X)` + the sequential sweep's order,
+ * kernel_matrix_factorization.py:369-425).  The visit order is cut into
+ * n_chunks contiguous chunks (<= 0: min(16, cores) from 2^20 ratings, else
+ * 1) levelled on as many threads, each chunk's levels placed after all of
+ * the earlier chunks'.  Every level is conflict-free and every rating's
+ * level is above each earlier rating of its user and item, so the levels
+ * applied in order (mf_sgd_epoch) give the same bits as mf_sched_levels'
+ * greedy levels -- more levels (the sum of the chunk depths), built in a
+ * fraction of the time.  order: 32-bit rating indices, n < 2^31.
+ * sched_out[lo_c, hi_c) holds chunk c's ratings (the chunk's own range of
+ * visit positions), by level, each level in visit order.
+ */
+int mf_sched_levels_chunked(const int32_t* user_ids, const int32_t* item_ids,
+                            int64_t n, const int32_t* order, int32_t n_users,
+                            int32_t n_items, int32_t use_user, int32_t use_item,
+                            int32_t n_chunks, int32_t* sched_out, int64_t* level_offsets,
+                            int64_t offsets_cap, int32_t* n_levels_out);
+
+/*
  * Throughput schedule.  Greedy edge colouring of the bipartite rating graph
  * (no two ratings of one colour share a user or an item), ratings visited
  * item by item.  Output: rating indices grouped by colour, each colour sorted
@@ -596,6 +623,11 @@ void mf_strata_plan_free(mf_strata_plan* plan);
  *     elem_bytes 4 or 8.
  * Threads: min(16, cores) unless MF_HOST_THREADS is set. */
 int mf_legacy_shuffle(uint32_t* mt_key, int32_t* mt_pos, int64_t* data, int64_t n);
+/* mf_legacy_shuffle on a 1-D array of 4-byte elements: the same draws and
+ * swaps (they depend on n only), half the bytes moved; the exact schedule's
+ * per-epoch np.random.shuffle of the row order (kernel_matrix_factorization.py:371)
+ * runs on 32-bit rating indices. */
+int mf_legacy_shuffle_i32(uint32_t* mt_key, int32_t* mt_pos, int32_t* data, int64_t n);
 int mf_legacy_permutation(uint32_t* mt_key, int32_t* mt_pos, int64_t* out, int64_t n);
 int mf_pairs_duplicated(const int64_t* a, const int64_t* b, int64_t n, int32_t* has_dup);
 int mf_factorize(const int64_t* vals, int64_t n, int64_t* codes, int64_t* uniques,

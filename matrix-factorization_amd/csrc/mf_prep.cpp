@@ -166,6 +166,21 @@ extern "C" int mf_legacy_shuffle(uint32_t* mt_key, int32_t* mt_pos, int64_t* dat
     return MF_OK;
 }
 
+// np.random.shuffle of a 1-D array of 4-byte elements (the same draws and
+// swaps as mf_legacy_shuffle: the swap targets depend on n only)
+extern "C" int mf_legacy_shuffle_i32(uint32_t* mt_key, int32_t* mt_pos, int32_t* data, int64_t n) {
+    if (!mt_key || !mt_pos || (n > 0 && !data) || n < 0) {
+        set_error("mf_legacy_shuffle_i32: null pointer or negative n");
+        return MF_ERR_INVALID;
+    }
+    MT mt;
+    if (const int rc = load_mt(mt, mt_key, mt_pos, n, "mf_legacy_shuffle_i32")) return rc;
+    shuffle_raw(mt, data, n);
+    std::memcpy(mt_key, mt.key, sizeof(mt.key));
+    *mt_pos = mt.pos;
+    return MF_OK;
+}
+
 // np.random.permutation(n): the shuffle of arange(n) run on 4-byte elements
 // while n < 2^31 (the same draws and swaps on half the bytes), widened into
 // out afterwards.

@@ -1,7 +1,6 @@
 // mf_rows_f32.hip -- float instantiations of the SGD-batch and SSE kernels
 // (split per dtype so the two halves compile in parallel).
 #include "mf_rows.hpp"
-#include "mf_strata.hpp"
 
 namespace mf {
 
@@ -15,9 +14,5 @@ int sse_launch_f32(const SseParams& p) {
     return dispatch_rows<float>(p.k, p.kernel, r);
 }
 
-int strata_launch_f32(const StrataParams& p) {
-    StrataRun<float> r{p};
-    return dispatch_rows<float>(p.k, p.kernel, r);
-}
 
 }  // namespace mf

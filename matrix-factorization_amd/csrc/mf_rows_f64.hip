@@ -1,7 +1,6 @@
 // mf_rows_f64.hip -- double instantiations of the SGD-batch and SSE kernels
 // (split per dtype so the two halves compile in parallel).
 #include "mf_rows.hpp"
-#include "mf_strata.hpp"
 
 namespace mf {
 
@@ -15,9 +14,5 @@ int sse_launch_f64(const SseParams& p) {
     return dispatch_rows<double>(p.k, p.kernel, r);
 }
 
-int strata_launch_f64(const StrataParams& p) {
-    StrataRun<double> r{p};
-    return dispatch_rows<double>(p.k, p.kernel, r);
-}
 
 }  // namespace mf

@@ -875,6 +875,400 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_epoch(StrataArgs<T> A
         strata_store_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
 }
 
+// ---------------------------------------------------------------------------
+// The stream form of the multi-class persistent epoch (MF_FLAG_STREAM; C > 1,
+// the depth-2 pipeline).  k_sgd_strata_epoch runs each position (block) as
+// its own software pipeline: a prologue of two dependent global round trips
+// (the block's triples, then its user rows) and the user-bias slice staged
+// behind them, then the steps, then a drain -- at C3 with 4 classes the
+// blocks are 6.45 steps long and that prologue is ~1.9 us of a 12 us
+// position ("stream").  Here ONE pipeline runs through
+// all positions of the launch: the triples are loaded 4 steps ahead and the
+// user rows gathered 2 steps ahead across block boundaries, so the next
+// block's first rows are in flight while the current block's last steps
+// apply.  What a boundary still needs:
+//  * the next position's user range released by its previous holder (C
+//    positions back, another workgroup): polled every step from the start
+//    of the current block (one sc1 load per wave, its value read two steps
+//    later); the wave that has not seen it released by the step whose gathers
+//    enter the next block spins there (per wave: a wave's rows are its own
+//    slots', nothing else of the wave depends on other waves);
+//  * the next block's user-bias slice, staged into the other of two LDS
+//    slices: its sc1 loads issued with those first gathers, written to LDS
+//    at the end of the next step (one barrier before the block's first
+//    step); the finished slice is stored back (write-through) at the first
+//    step of the following block;
+//  * the hand-off: a drain (vmcnt(0)), a barrier and one flag store at the
+//    end of the SECOND step of a block, publishing every position before it
+//    -- taken every D = C - 1 positions as in k_sgd_strata_epoch.  A wait
+//    (at step nv - 2 >= 2 of position p, for position p + 1) depends only on
+//    publications made at step 1 of positions <= p by other workgroups,
+//    which precede their own waits: no cycle.
+// Blocks shorter than kStreamMinSteps are run with idle steps added (no
+// load, no store), so the lookahead of 4 steps never crosses two
+// boundaries.  Every global load and store is issued on every step (a
+// dropped buffer offset when not needed) and every loaded register is
+// consumed on every step, so the compiler's memory-counter waits stay exact
+// (a load consumed on some paths only costs a full drain).  The same
+// sequential order as k_sgd_strata_epoch (bit for bit; tests/test_gpu_strata.py).
+constexpr int kStreamMinSteps = 4;
+
+// geometry of one position (LDS table built at the start of the launch)
+struct StreamGeo {
+    int st0, nst, rot, nv, ulo, nus, wd;
+};
+
+template <typename T>
+__host__ __device__ inline size_t strata_stream_lds_bytes(int max_items, int cap, int k, int th,
+                                                          int n_seq) {
+    const size_t tb = sizeof(T) * ((size_t)max_items * (size_t)k + (size_t)max_items +
+                                   2 * (size_t)cap + (size_t)th);
+    return ((tb + 15) / 16) * 16 + 16 * (size_t)n_seq;
+}
+
+template <typename T, int W, int GS, int V, int KERN, int S, int NW, int KB>
+__global__ __launch_bounds__(NW * kWave) void k_sgd_strata_stream(StrataArgs<T> A,
+                                                                     const StrataSeq seq,
+                                                                     int32_t n_seq, int32_t* done,
+                                                                     int32_t* err, int32_t cap) {
+    using VT = typename VecOf<T, W>::type;
+    constexpr int TH = NW * kWave;
+    constexpr int R = kWave / GS;
+    constexpr int RPW = S * R;
+    constexpr int NS = NW * RPW;
+    constexpr bool BIAS = KERN != MF_RBF;
+    extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int s_base;
+    const int B = A.B, C = A.cls;
+    const int w = blockIdx.x;
+    const int ilo = A.ibnd[w], nqi = A.ibnd[w + 1] - ilo;
+    const int k = A.k;
+    const int kv = k / W;
+    T* Qs = reinterpret_cast<T*>(smem);
+    T* Bis = Qs + (size_t)nqi * k;
+    T* Bus = Bis + nqi;                  // two slices of `cap`
+    T* Dum = Bus + 2 * (size_t)cap;      // one dummy entry per thread
+    // the geometry table follows this workgroup's slab and slices (16-B
+    // aligned); the launcher sized the LDS for the largest slab
+    const size_t gofs = ((sizeof(T) * ((size_t)nqi * k + nqi + 2 * (size_t)cap + TH) + 15) / 16) * 16;
+    int4* Geo = reinterpret_cast<int4*>(smem + gofs);
+    if (threadIdx.x == 0)
+        s_base = __hip_atomic_load(done + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const Hyper<T> h = hyper_regs(A.h);
+    strata_stage_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
+    for (int p = threadIdx.x; p < n_seq; p += TH) {
+        const int s = seq.s[p];
+        const int64_t blk = (int64_t)s * B + w;
+        const int64_t st0 = A.bstep[blk];
+        const int nst = (int)(A.bstep[blk + 1] - st0);
+        if (nst > 0xFFFF && err)       // (16-bit table entry: the caller replays per stratum)
+            __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int rot = nst > 0 ? (int)(strata_mix(A.seed, (uint32_t)blk) % (uint32_t)nst) : 0;
+        const int ub = (s + C * w) % (C * B);
+        const int ulo = A.ubnd[ub], nus = A.ubnd[ub + 1] - ulo;
+        const int wd = p >= C ? (w + s / C - (int)seq.s[p - C] / C + 2 * B) % B : 0;
+        Geo[p] = make_int4((int)st0, (nst & 0xFFFF) | (rot << 16), ulo,
+                           (nus & 0xFFFFFF) | (wd << 24));
+    }
+    __syncthreads();
+    const int base = s_base;
+
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wv = threadIdx.x / kWave;
+    const int g = lane / GS;
+    const int l = lane % GS;
+    const uint32_t lslot = (uint32_t)(wv * RPW + (lane < RPW ? lane : 0));
+    const uint32_t kb = (uint32_t)k * (uint32_t)sizeof(T);
+    const __amdgpu_buffer_rsrc_t prs = buf_rsrc(A.P, A.p_bytes);
+    const __amdgpu_buffer_rsrc_t tru = buf_rsrc(A.u, A.tri_bytes);
+    const __amdgpu_buffer_rsrc_t tri = buf_rsrc(A.i, A.tri_bytes);
+    const __amdgpu_buffer_rsrc_t trr =
+        buf_rsrc(A.r, (uint64_t)A.tri_bytes / sizeof(int32_t) * sizeof(T));
+    [[maybe_unused]] const __amdgpu_buffer_rsrc_t brs = buf_rsrc(A.Bu, A.bu_bytes);
+    const __amdgpu_buffer_rsrc_t drs = buf_rsrc(done, (uint64_t)B * sizeof(int32_t));
+
+    auto rfl = [](int v) __attribute__((always_inline)) { return __builtin_amdgcn_readfirstlane(v); };
+    auto geo = [&](int p) __attribute__((always_inline)) {
+        StreamGeo q;
+        if (p < n_seq) {
+            const int4 e = Geo[p];
+            q.st0 = rfl(e.x);
+            const uint32_t y = (uint32_t)rfl(e.y), z = (uint32_t)rfl(e.w);
+            q.nst = (int)(y & 0xFFFFu);
+            q.rot = (int)(y >> 16);
+            q.ulo = rfl(e.z);
+            q.nus = (int)(z & 0xFFFFFFu);
+            q.wd = (int)(z >> 24);
+        } else {
+            q.st0 = q.nst = q.rot = q.ulo = q.nus = q.wd = 0;
+        }
+        q.nv = q.nst > kStreamMinSteps ? q.nst : kStreamMinSteps;
+        return q;
+    };
+    // cursors: apply at (pA, jA); geometry of pA - 1, pA, pA + 1, pA + 2
+    int pA = 0, jA = 0;
+    StreamGeo gP = geo(n_seq);           // (empty)
+    StreamGeo gA = geo(0), gN = geo(1), gNN = geo(2);
+    bool relN = true;                    // position pA + 1 needs no (more) waiting
+    const int D = C > 1 ? C - 1 : 1;
+    int nextsig = D - 1;                 // publish after this position
+
+    struct Tri { int u, i; T r; bool real; };
+    struct Rows { int u[S], i[S]; bool have[S]; T r[S]; VT p[S][V]; };
+    struct Stage { T v[KB]; bool on; };
+    struct Poll { int v; int p; };
+
+    // triples of the step `d` ahead of the apply cursor (d <= 4: at most one
+    // boundary ahead, since every position has >= 4 steps)
+    auto load_tri = [&](int d, Tri& o) __attribute__((always_inline)) {
+        int j = jA + d;
+        const bool nx = j >= gA.nv;
+        if (nx) j -= gA.nv;
+        const int nst = nx ? gN.nst : gA.nst;
+        const int rot = nx ? gN.rot : gA.rot;
+        const int st0 = nx ? gN.st0 : gA.st0;
+        const bool real = j < nst;
+        int c = rot + j;
+        if (c >= nst) c -= nst;
+        const uint32_t e = (uint32_t)(st0 + c) * (uint32_t)NS + lslot;        // < 2^30
+        o.u = buf_ld<2, int>(tru, real ? e * 4u : kBufDrop);
+        o.i = buf_ld<2, int>(tri, real ? e * 4u : kBufDrop);
+        o.r = buf_ld<2, T>(trr, real ? e * (uint32_t)sizeof(T) : kBufDrop);
+        o.real = real;
+    };
+    auto unpack_gather = [&](const Tri& tr, Rows& o, auto full) __attribute__((always_inline)) {
+        constexpr bool FULL = decltype(full)::value;
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+            const int src = x * R + g;
+            const int uv = take_i<GS>(tr.u, src);
+            const int iv = take_i<GS>(tr.i, src);
+            o.have[x] = tr.real && uv >= 0;
+            o.u[x] = o.have[x] ? uv : 0;                   // idle: row 0, never stored
+            o.i[x] = o.have[x] ? iv - ilo : 0;
+            o.r[x] = take_f<GS>(tr.r, src);
+        }
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const int vi = v * GS + l;
+                const int vc = FULL || vi < kv ? vi : kv - 1;
+                o.p[x][v] = buf_ld<16, VT>(
+                    prs, mad_u24((uint32_t)o.u[x], kb, (uint32_t)(vc * W * (int)sizeof(T))));
+            }
+        }
+    };
+    auto qrow = [&](int i) __attribute__((always_inline)) -> VT* {
+        return reinterpret_cast<VT*>(reinterpret_cast<char*>(Qs) + mad_u24((uint32_t)i, kb, 0u));
+    };
+    int uprev[S], uprev2[S];
+    VT pprev[S][V], pprev2[S][V];
+#pragma unroll
+    for (int x = 0; x < S; ++x) uprev[x] = uprev2[x] = -1;
+
+    // one step: rows of g+2 gathered from Tc, triples of g+4 -> Tn, apply Ra;
+    // staging loads -> Sn, staged values of the last step (Sp) -> LDS; poll
+    // -> Pn, the poll of two steps ago (Po) read
+    auto step = [&](Tri& Tc, Tri& Tn, Rows& Ra, Rows& Rc, Stage& Sn, Stage& Sp, Poll& Pn,
+                    Poll& Po, auto full) __attribute__((always_inline)) {
+        constexpr bool FULL = decltype(full)::value;
+        // (1) the poll issued two steps ago: next range released?
+        {
+            const int pv = rfl(Po.v);
+            if (!relN && Po.p == pA + 1 && pv >= base + pA + 2 - C) relN = true;
+        }
+        // (2) the first gathers of position pA + 1 are issued this step: its
+        // user range must be released (per wave)
+        const bool enter = jA + 2 == gA.nv;
+        if (enter && !relN) {
+            const int tgt = base + pA + 2 - C;
+            int64_t spins = 0;
+            while (rfl(buf_ld<16, int>(drs, (uint32_t)gN.wd * 4u)) < tgt) {
+                if (++spins > kStrataSpinLimit ||
+                    __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                    if (lane == 0)
+                        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            relN = true;
+            // every load of handed-off bytes below is sc1 (no stale L1 line):
+            // only keep the compiler from hoisting them above the poll
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        // (3) loads, oldest first: staging of the next slice, the poll, the
+        // rows of g+2, the triples of g+4
+        if constexpr (BIAS) {
+            const bool on = enter && pA + 1 < n_seq;
+            Sn.on = on;
+#pragma unroll
+            for (int q = 0; q < KB; ++q) {
+                const int x = (int)threadIdx.x + q * TH;
+                const bool ok = on && x < gN.nus;
+                Sn.v[q] = buf_ld<16, T>(brs, ok ? (uint32_t)(gN.ulo + x) * (uint32_t)sizeof(T)
+                                              : kBufDrop);
+            }
+        }
+        {
+            const bool need = !relN && pA + 1 < n_seq;
+            Pn.p = pA + 1;
+            Pn.v = buf_ld<16, int>(drs, need ? (uint32_t)gN.wd * 4u : kBufDrop);
+        }
+        unpack_gather(Tc, Rc, full);
+        load_tri(4, Tn);
+        // (4) apply the rows of this step
+        const int bofs = (pA & 1) * cap - gA.ulo;
+        VT p[S][V], q[S][V];
+        T bu[S], bi[S];
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+            const bool f1 = uprev[x] == Ra.u[x];
+            const bool f2 = !f1 && uprev2[x] == Ra.u[x];
+            const VT* row = qrow(Ra.i[x]);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const int vi = v * GS + l;
+                const bool in = FULL || vi < kv;
+                const VT qv = row[in ? vi : kv - 1];
+                p[x][v] = in ? (f1 ? pprev[x][v] : (f2 ? pprev2[x][v] : Ra.p[x][v])) : (VT)(T)0;
+                q[x][v] = in ? qv : (VT)(T)0;
+            }
+            if constexpr (BIAS) {
+                bu[x] = Bus[Ra.have[x] ? Ra.u[x] + bofs : 0];
+                bi[x] = Bis[Ra.i[x]];
+            } else {
+                bu[x] = bi[x] = (T)0;
+            }
+        }
+#pragma unroll
+        for (int x = 0; x < S; ++x) {
+            const T sm = group_sum<GS>(lane_partial<T, W, V, KERN, true>(p[x], q[x]));
+            T e, d;
+            sgd_error<T, KERN>(sm, bu[x], bi[x], Ra.r[x], h, e, d);
+            const bool lead = Ra.have[x] && l == 0;
+            if constexpr (BIAS) {
+                if (A.upd_user && lead) Bus[Ra.u[x] + bofs] = sgd_bias<T, KERN>(bu[x], e, d, h);
+                if (A.upd_item && lead) Bis[Ra.i[x]] = sgd_bias<T, KERN>(bi[x], e, d, h);
+            }
+            VT* qw = qrow(Ra.i[x]);
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                const int vi = v * GS + l;
+                VT np, nq;
+                sgd_rows<T, KERN>(p[x][v], q[x][v], e, d, h, np, nq);
+                pprev2[x][v] = pprev[x][v];
+                pprev[x][v] = np;
+                const bool ok = Ra.have[x] && (FULL || vi < kv);
+                const uint32_t off = (ok && A.upd_user)
+                    ? mad_u24((uint32_t)Ra.u[x], kb, (uint32_t)(vi * W * (int)sizeof(T)))
+                    : kBufDrop;
+                buf_st<16>(prs, off, np);
+                if (ok && A.upd_item) qw[vi] = nq;
+            }
+            uprev2[x] = uprev[x];
+            uprev[x] = (Ra.have[x] && A.upd_user) ? Ra.u[x] : -1;
+        }
+        if constexpr (BIAS) {
+            // (5) the previous position's slice back to memory (write-through),
+            // at the first step of this one
+            const bool wb = jA == 0 && pA >= 1 && pA < n_seq && A.upd_user;
+            const int sb = ((pA + 1) & 1) * cap;           // = slice of pA - 1
+#pragma unroll
+            for (int q2 = 0; q2 < KB; ++q2) {
+                const int x = (int)threadIdx.x + q2 * TH;
+                const T v = Bus[sb + (x < cap ? x : cap - 1)];
+                buf_st<16>(brs, (wb && x < gP.nus) ? (uint32_t)(gP.ulo + x) * (uint32_t)sizeof(T)
+                                                  : kBufDrop, v);
+            }
+            // (6) the slice staged last step into the next position's LDS
+            // slice (a dummy entry when nothing was staged)
+            const int nb = ((pA + 1) & 1) * cap;
+#pragma unroll
+            for (int q2 = 0; q2 < KB; ++q2) {
+                const int x = (int)threadIdx.x + q2 * TH;
+                T* dst = (Sp.on && x < cap) ? &Bus[nb + x] : &Dum[threadIdx.x];
+                *dst = Sp.v[q2];
+            }
+        }
+        lds_barrier();
+        // (7) publish: every position before pA is complete (its rows were
+        // stored before this point, its bias slice at step 0)
+        if (jA == 1 && pA >= 1 && pA < n_seq && pA - 1 == nextsig) {
+            nextsig += D;
+            __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
+            __syncthreads();
+            if (threadIdx.x == 0)
+                __hip_atomic_store(done + w, base + pA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // (8) advance the apply cursor
+        if (++jA == gA.nv) {
+            ++pA;
+            jA = 0;
+            gP = gA;
+            gA = gN;
+            gN = gNN;
+            gNN = geo(pA + 2);
+            relN = pA + 1 < C || pA + 1 >= n_seq;
+        }
+    };
+
+    // prologue: position 0's bias slice staged; triples of steps 0..3, rows
+    // of steps 0 and 1
+    Tri ta, tb, tc;
+    Rows ra, rb, rc;
+    Stage sa, sb, sc;
+    Poll pa, pb, pc;
+    sa.on = sb.on = sc.on = false;
+    pa.p = pb.p = pc.p = -1;
+#pragma unroll
+    for (int q = 0; q < KB; ++q) sa.v[q] = sb.v[q] = sc.v[q] = (T)0;
+    pa.v = pb.v = pc.v = 0;
+    load_tri(0, ta);
+    load_tri(1, tb);
+    load_tri(2, tc);
+    unpack_gather(ta, ra, std::false_type{});
+    load_tri(3, ta);
+    unpack_gather(tb, rb, std::false_type{});
+    if constexpr (BIAS) {
+        if (n_seq > 0)
+            for (int x = threadIdx.x; x < gA.nus; x += TH)
+                Bus[x] = buf_ld<16, T>(brs, (uint32_t)(gA.ulo + x) * (uint32_t)sizeof(T));
+    }
+    lds_barrier();
+    auto run = [&](auto full) __attribute__((always_inline)) {
+        // copies by step mod 3 (no register with a load in flight is copied):
+        // step s applies R[s%3], gathers rows of s+2 from T[(s+2)%3] into
+        // R[(s+2)%3], loads triples of s+4 into T[(s+1)%3], stages into
+        // S[s%3] and writes S[(s+2)%3], polls into P[s%3] and reads P[(s+1)%3]
+        while (pA < n_seq) {
+            step(tc, tb, ra, rc, sa, sc, pa, pb, full);
+            step(ta, tc, rb, ra, sb, sa, pb, pc, full);
+            step(tb, ta, rc, rb, sc, sb, pc, pa, full);
+        }
+    };
+    if (kv == GS * V) run(std::true_type{});
+    else run(std::false_type{});
+    // epilogue: the last position's slice back, then publish the launch's end
+    if constexpr (BIAS) {
+        if (n_seq > 0 && A.upd_user) {
+            const StreamGeo gl = geo(n_seq - 1);
+            const int sb = ((n_seq - 1) & 1) * cap;
+            for (int x = threadIdx.x; x < gl.nus; x += TH)
+                buf_st<16>(brs, (uint32_t)(gl.ulo + x) * (uint32_t)sizeof(T), Bus[sb + x]);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(done + w, base + n_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (A.Dq)
+        strata_delta_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
+    else
+        strata_store_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
+}
+
 // Is `seq` an XCD-class order (engine.stratum_order "xcd"): B a multiple of
 // 8 and the strata of each class s mod 8 one contiguous run, every class
 // once?  Then a user range's holder changes XCD only between runs and meets
@@ -1096,7 +1490,30 @@ struct StrataRun {
                                    : k_sgd_strata_epoch<T, W, GS, V, KERN, S, 1, NW, false>);
             MF_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(efn),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-            persistent = strata_coresident(reinterpret_cast<const void*>(efn), p.B, lds, TH);
+            // the stream form (C > 1, depth-2 pipeline, MF_FLAG_STREAM): one
+            // software pipeline through the launch's positions
+            const void* sfn = nullptr;
+            size_t slds = 0;
+            int32_t cap = std::max(p.max_users, 1);
+            if constexpr (kDeep == 2 && V <= 2) {      // (rows of <= 2 vectors per lane)
+                if ((p.flags & MF_FLAG_STREAM) && deep && a.cls > 1 && p.B <= 256 &&
+                    cap <= 4 * TH) {
+                    slds = strata_stream_lds_bytes<T>(p.max_items, cap, p.k, TH, p.n_seq);
+                    if (slds <= (size_t)kLdsLimit)
+                        sfn = cap <= 2 * TH
+                                  ? reinterpret_cast<const void*>(
+                                        k_sgd_strata_stream<T, W, GS, V, KERN, S, NW, 2>)
+                                  : reinterpret_cast<const void*>(
+                                        k_sgd_strata_stream<T, W, GS, V, KERN, S, NW, 4>);
+                }
+            }
+            if (sfn) {
+                MF_HIP_CHECK(hipFuncSetAttribute(sfn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)slds));
+                persistent = strata_coresident(sfn, p.B, slds, TH);
+            } else {
+                persistent = strata_coresident(reinterpret_cast<const void*>(efn), p.B, lds, TH);
+            }
             if (persistent) {
                 int32_t* done = static_cast<int32_t*>(p.ws);
                 int32_t* err = done + p.B;
@@ -1115,7 +1532,21 @@ struct StrataRun {
                 if (strata_inject_fail())
                     MF_HIP_CHECK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(err), 1, 1,
                                                    p.stream));
-                if (p.flags & MF_FLAG_NO_COOP) {
+                if (sfn) {
+                    a.xtab = nullptr;            // (the L2 hand-off needs one class)
+                    void* kargs[] = {&a, &sq, &nseq, &done, &err, &cap};
+                    hipError_t ce;
+                    if (p.flags & MF_FLAG_NO_COOP)
+                        ce = hipLaunchKernel(sfn, dim3((unsigned)p.B), dim3(TH), kargs,
+                                             slds, p.stream);
+                    else
+                        ce = hipLaunchCooperativeKernel(sfn, dim3((unsigned)p.B), dim3(TH),
+                                                        kargs, (unsigned)slds, p.stream);
+                    if (ce != hipSuccess) {
+                        (void)hipGetLastError();
+                        persistent = false;
+                    }
+                } else if (p.flags & MF_FLAG_NO_COOP) {
                     hipLaunchKernelGGL(efn, dim3((unsigned)p.B), dim3(TH), lds,
                                        p.stream, a, sq, nseq, done, err);
                 } else {

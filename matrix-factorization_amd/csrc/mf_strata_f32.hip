@@ -1,0 +1,13 @@
+// mf_strata_f32.hip -- float instantiations of the stratified SGD kernels
+// (mf_strata.hpp), apart from the batch / SSE kernels so each compiles alone.
+#include "mf_rows.hpp"
+#include "mf_strata.hpp"
+
+namespace mf {
+
+int strata_launch_f32(const StrataParams& p) {
+    StrataRun<float> r{p};
+    return dispatch_rows<float>(p.k, p.kernel, r);
+}
+
+}  // namespace mf

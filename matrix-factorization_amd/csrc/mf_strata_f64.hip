@@ -1,0 +1,13 @@
+// mf_strata_f64.hip -- double instantiations of the stratified SGD kernels
+// (mf_strata.hpp), apart from the batch / SSE kernels so each compiles alone.
+#include "mf_rows.hpp"
+#include "mf_strata.hpp"
+
+namespace mf {
+
+int strata_launch_f64(const StrataParams& p) {
+    StrataRun<double> r{p};
+    return dispatch_rows<double>(p.k, p.kernel, r);
+}
+
+}  // namespace mf

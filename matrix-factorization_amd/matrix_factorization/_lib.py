@@ -26,6 +26,7 @@ MF_FLAG_NO_COOP = 64
 MF_FLAG_NARROW = 128
 MF_FLAG_L2_HANDOFF = 256
 MF_FLAG_NO_EARLY_POLL = 512
+MF_FLAG_STREAM = 1024
 MF_FLAG_CLASSES_SHIFT = 24       # bits 24..27: user-range classes - 1
 MF_STRATA_MAX_CLASSES = 4
 MF_ERR_CAPACITY = 3
@@ -108,6 +109,8 @@ SIGNATURES = {
     "mf_replica_apply": (ctypes.c_int, [_P, _P, _I64, _I32, _F64, _P]),
     "mf_sched_levels": (ctypes.c_int, [
         _P, _P, _I64, _P, _I32, _I32, _I32, _I32, _P, _P, _I64, _P]),
+    "mf_sched_levels_chunked": (ctypes.c_int, [
+        _P, _P, _I64, _P, _I32, _I32, _I32, _I32, _I32, _P, _P, _I64, _P]),
     "mf_sched_color": (ctypes.c_int, [
         _P, _P, _I64, _I32, _I32, _P, _P, _I64, _P]),
     "mf_sched_slices": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P, _P]),
@@ -121,6 +124,7 @@ SIGNATURES = {
     "mf_strata_set_probe": (ctypes.c_int, [_P]),
     "mf_strata_inject_fail": (ctypes.c_int, [_I32]),
     "mf_legacy_shuffle": (ctypes.c_int, [_P, _P, _P, _I64]),
+    "mf_legacy_shuffle_i32": (ctypes.c_int, [_P, _P, _P, _I64]),
     "mf_legacy_permutation": (ctypes.c_int, [_P, _P, _P, _I64]),
     "mf_pairs_duplicated": (ctypes.c_int, [_P, _P, _I64, _P]),
     "mf_factorize": (ctypes.c_int, [_P, _I64, _P, _P, _P]),

@@ -25,10 +25,12 @@ def _ptr(a: np.ndarray) -> int:
 
 
 def legacy_shuffle_(a: np.ndarray) -> None:
-    """``np.random.shuffle(a)`` for a 1-D contiguous 8-byte array, in place,
-    advancing the global RandomState exactly as NumPy does."""
-    if a.ndim != 1 or a.dtype.itemsize != 8 or not a.flags.c_contiguous \
-            or not a.flags.writeable or len(a) > _MAX_N:
+    """``np.random.shuffle(a)`` for a 1-D contiguous 8- or 4-byte array, in
+    place, advancing the global RandomState exactly as NumPy does (the swap
+    targets depend on len(a) only, so the element size changes nothing but
+    the bytes moved)."""
+    if a.ndim != 1 or a.dtype.itemsize not in (4, 8) or not a.flags.c_contiguous \
+            or not a.flags.writeable or len(a) > _MAX_N or a.dtype.hasobject:
         np.random.shuffle(a)
         return
     st = np.random.get_state()
@@ -37,8 +39,12 @@ def legacy_shuffle_(a: np.ndarray) -> None:
         return
     key = np.ascontiguousarray(st[1], dtype=np.uint32).copy()
     pos = ctypes.c_int32(int(st[2]))
-    _lib.call("mf_legacy_shuffle", _ptr(key), ctypes.addressof(pos),
-              _ptr(a.view(np.int64)), len(a))
+    if a.dtype.itemsize == 8:
+        _lib.call("mf_legacy_shuffle", _ptr(key), ctypes.addressof(pos),
+                  _ptr(a.view(np.int64)), len(a))
+    else:
+        _lib.call("mf_legacy_shuffle_i32", _ptr(key), ctypes.addressof(pos),
+                  _ptr(a.view(np.int32)), len(a))
     np.random.set_state(("MT19937", key, pos.value, st[3], st[4]))
 
 

@@ -98,6 +98,34 @@ def sched_levels(u: np.ndarray, i: np.ndarray, order: Optional[np.ndarray],
     return sched, offs[: nl.value + 1].copy()
 
 
+def sched_levels_chunked(u: np.ndarray, i: np.ndarray, order: np.ndarray,
+                         n_users: int, n_items: int, use_user: bool = True,
+                         use_item: bool = True, n_chunks: int = 0,
+                         out: Optional[np.ndarray] = None) -> Tuple[np.ndarray, np.ndarray]:
+    """Exact-order batches built on host threads (mf_sched_levels_chunked):
+    the visit order cut into ``n_chunks`` chunks (0 = by size), each levelled
+    alone and placed after the earlier chunks' levels -- the same sequential
+    sweep as ``sched_levels`` (bit for bit), more levels.  ``order``: 32-bit
+    rating indices.  ``out``: optional int32 buffer of n (e.g. pinned memory
+    for an asynchronous upload) that receives the schedule."""
+    n = len(u)
+    u = np.ascontiguousarray(u, np.int32)
+    i = np.ascontiguousarray(i, np.int32)
+    order = np.ascontiguousarray(order, np.int32)
+    if len(order) != n:
+        raise ValueError("order and ratings differ in length")
+    sched = np.empty(n, np.int32) if out is None else out
+    if sched.dtype != np.int32 or len(sched) < n or not sched.flags.c_contiguous:
+        raise ValueError("out must be a contiguous int32 array of n entries")
+    # a chunk's depth is at most its length: n levels at most
+    offs = np.empty(n + 1, np.int64)
+    nl = ctypes.c_int32(0)
+    _lib.call("mf_sched_levels_chunked", _np(u), _np(i), n, _np(order), n_users,
+              n_items, int(use_user), int(use_item), int(n_chunks), _np(sched), _np(offs),
+              len(offs), ctypes.byref(nl))
+    return sched[:n], offs[: nl.value + 1].copy()
+
+
 def sched_color(u: np.ndarray, i: np.ndarray, n_users: int,
                 n_items: int) -> Tuple[np.ndarray, np.ndarray]:
     """Edge-colouring batches: (rating indices colour-major, colour offsets)."""
@@ -1256,10 +1284,42 @@ class SGDEngine:
         if self.colored is not None or self.strata is not None:
             raise RuntimeError("engine holds permuted ratings; exact order "
                                "needs the original order")
+        if order is not None and order.dtype == np.int32 and self.n > 0:
+            return self._epoch_exact_chunked(order, lr, reg, update_user, update_item, timing)
         sched, offs = sched_levels(self.u_host, self.i_host, order, self.n_users,
                                    self.n_items, update_user, update_item)
         idx = torch.from_numpy(sched).to(self.dev)
         return self._run(idx, offs, None, lr, reg, update_user, update_item, 0, timing)
+
+    def _epoch_exact_chunked(self, order, lr, reg, update_user, update_item, timing):
+        """epoch_exact for a 32-bit visit order: the levels built on host
+        threads (sched_levels_chunked, the same bits as the greedy levels)
+        straight into one of two pinned buffers, uploaded asynchronously on
+        the launch stream (the host builds epoch e+1's levels while the GPU
+        still runs epoch e; a buffer is rewritten only once its last upload
+        has completed)."""
+        st = getattr(self, "_exact_bufs", None)
+        if st is None or st["host"][0].numel() < self.n:
+            st = {"host": [torch.empty(self.n, dtype=torch.int32, pin_memory=True)
+                           for _ in range(2)],
+                  "ev": [None, None], "flip": 0,
+                  "dev": torch.empty(self.n, dtype=torch.int32, device=self.dev)}
+            self._exact_bufs = st
+        k = st["flip"]
+        st["flip"] ^= 1
+        if st["ev"][k] is not None:
+            st["ev"][k].synchronize()
+        hb = st["host"][k]
+        _, offs = sched_levels_chunked(self.u_host, self.i_host, order, self.n_users,
+                                       self.n_items, update_user, update_item,
+                                       out=hb.numpy())
+        with torch.cuda.device(self.dev):
+            stream = torch.cuda.current_stream(self.dev)
+            st["dev"][: self.n].copy_(hb[: self.n], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            st["ev"][k] = ev
+        return self._run(st["dev"], offs, None, lr, reg, update_user, update_item, 0, timing)
 
     def epoch_colored(self, seq: Optional[np.ndarray], lr: float, reg: float,
                       update_user: bool = True, update_item: bool = True,
@@ -1651,6 +1711,10 @@ class _ErrorPoll:
         return self.ev is not None and self.ev.query() and int(self.host[0]) != 0
 
 
+# the exact schedule pipelines its per-epoch shuffle from this many ratings
+EXACT_PIPELINE_MIN = 1 << 20
+
+
 def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
                reg: float, update_user: bool = True, update_item: bool = True,
                verbose: int = 0, rng_order: Optional[np.ndarray] = None,
@@ -1674,9 +1738,30 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
     far is replayed with the same draws as one launch per stratum -- the
     same sequential orders, hence the same result (RuntimeWarning).
     """
+    exact_next = None
     if schedule == "exact":
-        order = (np.arange(engine.n, dtype=np.int64) if rng_order is None
-                 else rng_order)
+        # the row order as 32-bit indices (np.random.shuffle's draws depend on
+        # the length only): half the bytes per swap, and the chunked level
+        # builder's input
+        narrow = engine.n < (1 << 31)
+        dt = np.int32 if narrow else np.int64
+        order = (np.arange(engine.n, dtype=dt) if rng_order is None
+                 else np.array(rng_order, dtype=dt))
+        # epoch e+1's shuffle is drawn on a worker thread while epoch e's
+        # levels are built and launched (DESIGN.md section 5, "exact schedule
+        # at scale"); nothing else draws from the global RandomState inside
+        # the loop, so the draws are the reference's in the reference's
+        # order.  Joined before the end of every epoch; off with an on_epoch
+        # callback (it might draw) and for n >= 2^31.
+        pipeline = narrow and on_epoch is None and engine.n >= EXACT_PIPELINE_MIN
+        if pipeline:
+            exact_pool = ThreadPoolExecutor(1)
+            exact_spare = np.empty_like(order)
+
+            def shuffled_copy(src, dst):
+                np.copyto(dst, src)
+                _prep.legacy_shuffle_(dst)
+                return dst
     elif schedule == "colored":
         if engine.colored is None:
             engine.prepare_colored()
@@ -1712,8 +1797,18 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
         if poll is not None and persistent is None and poll.failed():
             replay_failed(epoch)                  # stop launching persistent sweeps now
         if schedule == "exact":
-            _prep.legacy_shuffle_(order)          # = np.random.shuffle(order)
-            engine.epoch_exact(order, lr, reg, update_user, update_item)
+            if exact_next is not None:            # drawn during the last epoch
+                spare, order = order, exact_next.result()
+                exact_spare, exact_next = spare, None
+            else:
+                _prep.legacy_shuffle_(order)      # = np.random.shuffle(order)
+            if pipeline and epoch + 1 < n_epochs:
+                exact_next = exact_pool.submit(shuffled_copy, order, exact_spare)
+            try:
+                engine.epoch_exact(order, lr, reg, update_user, update_item)
+            finally:
+                if exact_next is not None:
+                    exact_next.exception()        # joined: RNG consistent at the epoch end
         elif schedule == "colored":
             seq = np.random.permutation(nb).astype(np.int32)
             engine.epoch_colored(seq, lr, reg, update_user, update_item)
@@ -1734,6 +1829,8 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
             print("Epoch ", epoch + 1, "/", n_epochs, " -  train_rmse:", rmse)
         if on_epoch is not None:
             on_epoch(epoch)
+    if schedule == "exact" and pipeline:
+        exact_pool.shutdown()
     if snap0 is not None and persistent is None and engine.strata_failed():
         replay_failed(n_epochs)
         if verbose == 1:

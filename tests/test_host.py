@@ -173,10 +173,15 @@ class OracleEngine:
                     max_rating=self.max_rating)
 
     def epoch_exact(self, order, lr, reg, update_user=True, update_item=True):
-        from matrix_factorization.engine import sched_levels
+        from matrix_factorization.engine import sched_levels, sched_levels_chunked
 
-        sched, offs = sched_levels(self.u_host, self.i_host, order, self.n_users,
-                                   self.n_items, update_user, update_item)
+        if order.dtype == np.int32:      # the product's path: chunked levels (3 chunks)
+            sched, offs = sched_levels_chunked(self.u_host, self.i_host, order, self.n_users,
+                                               self.n_items, update_user, update_item,
+                                               n_chunks=3)
+        else:
+            sched, offs = sched_levels(self.u_host, self.i_host, order, self.n_users,
+                                       self.n_items, update_user, update_item)
         for b in range(len(offs) - 1):
             lvl = sched[offs[b]:offs[b + 1]].astype(np.int64)
             if self.kernel == "bias":
@@ -580,3 +585,67 @@ def test_bench_traffic_lookup_is_keyed_on_world_and_emulation():
                                        "k_sgd_strata_epoch") is None
     assert bench.traffic_from_profiles("c3", 1, "strata_persistent", "float32",
                                        "k_sgd_strata") is None     # another kernel
+
+
+@pytest.mark.parametrize("chunks", [1, 2, 5, 16])
+def test_chunked_levels_are_an_exact_schedule(chunks):
+    """mf_sched_levels_chunked: a permutation of the ratings whose levels are
+    conflict-free and respect every user's and item's visit order (so the
+    level-by-level sweep is the sequential sweep, bit for bit); one chunk is
+    exactly mf_sched_levels' greedy schedule."""
+    from matrix_factorization.engine import sched_levels, sched_levels_chunked
+
+    rs = np.random.RandomState(chunks)
+    nu, ni, n = 300, 120, 9000
+    keys = rs.choice(nu * ni, n, replace=False)
+    u, i = (keys // ni).astype(np.int32), (keys % ni).astype(np.int32)
+    u[:200] = 7                                   # a heavy user and item
+    i[200:400] = 3
+    keep = np.unique(u.astype(np.int64) * ni + i, return_index=True)[1]
+    u, i = u[np.sort(keep)], i[np.sort(keep)]
+    n = len(u)
+    order = rs.permutation(n).astype(np.int32)
+    for uu, ui in ((True, True), (True, False)):
+        s, o = sched_levels_chunked(u, i, order, nu, ni, uu, ui, n_chunks=chunks)
+        assert np.array_equal(np.sort(s), np.arange(n))
+        assert o[0] == 0 and o[-1] == n and np.all(np.diff(o) > 0)
+        if chunks == 1:
+            g, go = sched_levels(u, i, order.astype(np.int64), nu, ni, uu, ui)
+            assert np.array_equal(s, g) and np.array_equal(o, go)
+        pos = np.empty(n, np.int64)
+        pos[order] = np.arange(n)
+        lev = np.empty(n, np.int64)
+        for L in range(len(o) - 1):
+            lev[s[o[L]:o[L + 1]]] = L
+            assert np.all(np.diff(pos[s[o[L]:o[L + 1]]]) > 0)   # visit order inside a level
+        for ids in ((u, i) if ui else (u,)):
+            srt = np.lexsort((pos, ids))
+            same = ids[srt][1:] == ids[srt][:-1]
+            assert np.all(lev[srt][1:][same] > lev[srt][:-1][same])
+    with pytest.raises(Exception, match="out of range"):
+        bad = order.copy()
+        bad[5] = n + 3
+        sched_levels_chunked(u, i, bad, nu, ni, n_chunks=chunks)
+
+
+def test_exact_pipeline_draws_the_reference_shuffles(cpu_engine, monkeypatch):
+    """fit_epochs' exact schedule draws epoch e+1's np.random.shuffle on a
+    worker thread during epoch e: same model, same train_rmse and the same
+    global RandomState afterwards as the unpipelined loop."""
+    import matrix_factorization.engine as E
+    from matrix_factorization import KernelMF
+
+    d = load_golden("tiny_linear")
+    hp = golden_hp(d)
+    hp["verbose"] = 0
+    X = pd.DataFrame({"user_id": d["user_id"], "item_id": d["item_id"]})
+    out = []
+    for pipe_min in (1 << 40, 0):
+        monkeypatch.setattr(E, "EXACT_PIPELINE_MIN", pipe_min)
+        np.random.seed(int(d["seed"]))
+        m = KernelMF(**hp).fit(X, pd.Series(d["rating"]))
+        out.append((m.user_features.copy(), list(m.train_rmse), np.random.randint(0, 2**31 - 1)))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
+    assert out[0][2] == out[1][2]                  # the RNG stream afterwards
+    assert np.max(np.abs(out[1][0] - d["user_features"])) < 1e-12

@@ -1,10 +1,12 @@
 """Wall time of the public KernelMF.fit() at C3 scale, split by phase.
 
 Synthetic 1M x 100K, 100M ratings (bench.synth), rank 64, linear kernel,
-float32, strata schedule.  Phases are timed by wrapping the functions fit()
+float32 (--dtype), strata schedule (--schedule exact: the reference's own
+visit order, np.random.shuffle of the rows every epoch).  Phases are timed by wrapping the functions fit()
 calls (preprocessing, normal() initialisation is the remainder, engine
 upload + strata plan, SGD epochs incl. the RMSE passes, parameter download).
 Usage: python tools/fit_walltime.py [--epochs 20] [--nnz 100000000]
+       [--schedule strata|exact] [--dtype float32|float64]
 """
 
 import argparse
@@ -34,6 +36,8 @@ def main():
     ap.add_argument("--nnz", type=int, default=100_000_000)
     ap.add_argument("--users", type=int, default=1_000_000)
     ap.add_argument("--items", type=int, default=100_000)
+    ap.add_argument("--schedule", default="strata", choices=["strata", "exact"])
+    ap.add_argument("--dtype", default="float32", choices=["float32", "float64"])
     ap.add_argument("--pandas-prep", action="store_true",
                     help="force the pandas preprocessing path (reference-shaped)")
     args = ap.parse_args()
@@ -102,13 +106,28 @@ def main():
         ep_events.insert(0, ev0)
         return out
 
-    kmf.fit_epochs = timed("epochs", with_events)
+    exact = args.schedule == "exact"
+    ep_wall = []
+    if exact:
+        # no on_epoch hook here: it would turn off the exact schedule's
+        # pipelined shuffle (fit_epochs); the wall clock at each epoch's
+        # epoch_exact call instead (no synchronisation)
+        inner_ex = SGDEngine.epoch_exact
+
+        def epoch_exact(self, *a, **kw):
+            ep_wall.append(time.perf_counter())
+            return inner_ex(self, *a, **kw)
+
+        SGDEngine.epoch_exact = epoch_exact
+        kmf.fit_epochs = timed("epochs", inner)
+    else:
+        kmf.fit_epochs = timed("epochs", with_events)
     SGDEngine.prepare_strata = timed("strata_plan", SGDEngine.prepare_strata)
     SGDEngine.snapshot_params = timed("start_snapshot", SGDEngine.snapshot_params)
     KernelMF._sync_params = timed("download", KernelMF._sync_params)
     torch.zeros(1, device="cuda:0")
     m = KernelMF(n_factors=64, n_epochs=args.epochs, lr=0.01, reg=0.02, verbose=0,
-                 min_rating=1, max_rating=5, dtype="float32", schedule="strata")
+                 min_rating=1, max_rating=5, dtype=args.dtype, schedule=args.schedule)
     np.random.seed(0)
     t = time.perf_counter()
     m.fit(X, y)
@@ -117,6 +136,27 @@ def main():
     # wall time from the end of preprocessing to the first epoch: the normal
     # draws on this thread beside the engine build on the worker
     phases["init_beside_engine_build"] = marks["epochs_start"] - marks["preprocess_end"]
+    if exact:
+        ep_wall.append(marks["epochs_end"])
+        out = {"what": "KernelMF.fit wall time, schedule='exact' (the reference's visit "
+                       "order: np.random.shuffle of the rows every epoch)",
+               "nnz": args.nnz, "n_users": m.n_users, "n_items": m.n_items,
+               "epochs": args.epochs, "dtype": args.dtype,
+               "fit_s": round(total, 3), "epochs_s": round(phases["epochs"], 3),
+               "epoch_s_mean": round(phases["epochs"] / args.epochs, 4),
+               "epoch_wall_s": [round(b - a, 4) for a, b in zip(ep_wall[:-1], ep_wall[1:])],
+               "epoch_wall_note": ("wall clock between consecutive epoch_exact calls (the "
+                                   "last: to the end of fit_epochs, RMSE read-back "
+                                   "included); epoch e+1's shuffle is drawn on a worker "
+                                   "thread while epoch e's levels are built and launched"),
+               "phases_s": {k: round(v, 3) for k, v in phases.items()},
+               "prep_calls_s": {k: round(v, 3) for k, v in calls.items()},
+               "final_train_rmse": float(m.train_rmse[-1]),
+               "train_rmse": [float(x) for x in m.train_rmse],
+               "host_threads": os.environ.get("MF_HOST_THREADS") or min(16, os.cpu_count()),
+               "synth_s": round(t_synth, 1)}
+        print(json.dumps(out))
+        return
     ep_ms = [a.elapsed_time(b) for a, b in zip(ep_events[:-1], ep_events[1:])]
     # the bench's timed loop (bench.py: epoch_strata + sse_async, events
     # around the whole step) on the SAME engine and plan after fit(): tells
