@@ -914,7 +914,8 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
                       f"threads/workgroup{', narrow lane groups' if plan.narrow else ''}) x "
                       f"{int(plan.n_steps.max())} steps max "
                       f"per block, {fill:.1%} slot fill"
-                      f"{', user rows 2 steps ahead' if eng._deep_pipe(plan) else ''})")
+                      f"{', user rows 2 steps ahead' if eng._deep_pipe(plan) else ''}"
+                      f"{', one pipeline through all positions (stream)' if (eng._deep_pipe(plan) and cls > 1 and eng._stream()) else ''})")
     else:
         nb = eng.prepare_colored()
         n_phases = 1

@@ -95,11 +95,25 @@ enum {
        (mf_strata_plan_build_classes; 0 = C = 1, the plain B x B plan) */
     MF_FLAG_CLASSES_SHIFT = 24
 };
+/* Jobs of one mf_permute_rows launch. */
+#define MF_PERMUTE_MAX_JOBS 4
 /* Largest number of user-range classes a strata plan may have. */
 #define MF_STRATA_MAX_CLASSES 4
 
 const char* mf_last_error(void);
 int mf_abi_version(void);
+/* One empty kernel launch on `stream`: makes the runtime load this library's
+ * code object for the current device now (the engine calls it while it is
+ * built) instead of inside the first training epoch. */
+int mf_warmup(void* stream);
+/* Up to MF_PERMUTE_MAX_JOBS row arrays permuted in one launch (the relabelled
+ * strata plans' parameter moves): job j has n_rows[j]
+ * rows of row_bytes[j] bytes (a multiple of 4); mode 0 gathers dst[r] =
+ * src[idx[r]], mode 1 scatters dst[idx[r]] = src[r].  DEVICE pointers in
+ * HOST arrays of n_jobs; idx[j] has n_rows[j] entries in [0, n_rows[j]). */
+int mf_permute_rows(int32_t n_jobs, void* const* dst, const void* const* src,
+                    const int64_t* const* idx, const int64_t* n_rows,
+                    const int32_t* row_bytes, int32_t mode, void* stream);
 /* Largest n_factors the kernels accept (inclusive). */
 int mf_max_factors(void);
 

@@ -339,3 +339,82 @@ extern "C" int mf_replica_delta(void* cur, const void* base, int64_t n, int32_t 
     MF_HIP_CHECK(hipGetLastError());
     return MF_OK;
 }
+
+// ---------------------------------------------------------------------------
+// Relabelled strata plans (engine._epoch_regroup): the
+// parameters move into a plan's labelling and back -- up to 4 row arrays (P,
+// Q, b_u, b_i) permuted in ONE launch.  Job j: rows of row_bytes[j] bytes;
+// gather (mode 0): dst[r] = src[idx[r]], scatter (mode 1): dst[idx[r]] =
+// src[r].  16-B accesses where a row is a whole number of them, else 8 / 4 B.
+namespace mf {
+struct PermJobs {
+    const char* src[MF_PERMUTE_MAX_JOBS];
+    char* dst[MF_PERMUTE_MAX_JOBS];
+    const int64_t* idx[MF_PERMUTE_MAX_JOBS];
+    int64_t rows[MF_PERMUTE_MAX_JOBS];
+    int32_t row_bytes[MF_PERMUTE_MAX_JOBS];
+    int32_t n;
+    int32_t mode;
+};
+
+template <typename V>
+__device__ __forceinline__ void permute_job(const PermJobs& J, int j, int64_t t0, int64_t stride) {
+    const int per = J.row_bytes[j] / (int)sizeof(V);               // vectors per row
+    const int64_t total = J.rows[j] * per;
+    const V* src = reinterpret_cast<const V*>(J.src[j]);
+    V* dst = reinterpret_cast<V*>(J.dst[j]);
+    for (int64_t t = t0; t < total; t += stride) {
+        const int64_t r = t / per;
+        const int c = (int)(t - r * per);
+        const int64_t o = J.idx[j][r];
+        if (J.mode == 0) dst[r * per + c] = src[o * per + c];
+        else dst[o * per + c] = src[r * per + c];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_permute_rows(PermJobs J) {
+    const int j = blockIdx.y;
+    const int64_t t0 = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    const int rb = J.row_bytes[j];
+    const uintptr_t al = reinterpret_cast<uintptr_t>(J.src[j]) | reinterpret_cast<uintptr_t>(J.dst[j]);
+    if (rb % 16 == 0 && al % 16 == 0) permute_job<uint4>(J, j, t0, stride);
+    else if (rb % 8 == 0 && al % 8 == 0) permute_job<uint2>(J, j, t0, stride);
+    else permute_job<uint32_t>(J, j, t0, stride);
+}
+}  // namespace mf
+
+extern "C" int mf_permute_rows(int32_t n_jobs, void* const* dst, const void* const* src,
+                               const int64_t* const* idx, const int64_t* n_rows,
+                               const int32_t* row_bytes, int32_t mode, void* stream) {
+    if (n_jobs < 0 || n_jobs > MF_PERMUTE_MAX_JOBS || (mode != 0 && mode != 1) ||
+        (n_jobs > 0 && (!dst || !src || !idx || !n_rows || !row_bytes))) {
+        set_error("mf_permute_rows: bad arguments");
+        return MF_ERR_INVALID;
+    }
+    PermJobs J{};
+    J.mode = mode;
+    int64_t most = 0;
+    for (int32_t j = 0; j < n_jobs; ++j) {
+        if (n_rows[j] < 0 || row_bytes[j] <= 0 || row_bytes[j] % 4 != 0 ||
+            (n_rows[j] > 0 && (!dst[j] || !src[j] || !idx[j]))) {
+            set_error("mf_permute_rows: job %d invalid", j);
+            return MF_ERR_INVALID;
+        }
+        if (n_rows[j] == 0) continue;
+        J.src[J.n] = static_cast<const char*>(src[j]);
+        J.dst[J.n] = static_cast<char*>(dst[j]);
+        J.idx[J.n] = idx[j];
+        J.rows[J.n] = n_rows[j];
+        J.row_bytes[J.n] = row_bytes[j];
+        most = std::max<int64_t>(most, n_rows[j] * (row_bytes[j] / 4));
+        ++J.n;
+    }
+    if (J.n == 0) return MF_OK;
+    const int64_t need = (most / 4 + kBlock - 1) / kBlock;            // ~one 16-B access per thread
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>(need, 8192));
+    hipLaunchKernelGGL(k_permute_rows, dim3(g, (unsigned)J.n), dim3(kBlock), 0,
+                       (hipStream_t)stream, J);
+    MF_HIP_CHECK(hipGetLastError());
+    return MF_OK;
+}

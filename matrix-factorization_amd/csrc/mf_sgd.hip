@@ -283,6 +283,17 @@ extern "C" size_t mf_strata_workspace_bytes(int32_t n_blocks, int32_t n_seq) {
     return n_blocks > 0 && n_seq >= 0 ? strata_ws_bytes(n_blocks, n_seq) : 0;
 }
 
+// One empty launch: the runtime loads the library's code object for the
+// device at the first launch of any of its kernels (tens of ms for this
+// library), which otherwise lands in the first training epoch.
+__global__ void k_warmup() {}
+
+extern "C" int mf_warmup(void* stream) {
+    hipLaunchKernelGGL(k_warmup, dim3(1), dim3(64), 0, (hipStream_t)stream);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MF_OK : hip_fail(e, "mf_warmup");
+}
+
 extern "C" int mf_strata_status(const void* workspace, int32_t n_blocks, void* stream) {
     if (!workspace || n_blocks < 1) {
         set_error("mf_strata_status: NULL workspace");

@@ -952,11 +952,20 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_stream(StrataArgs<T> 
     // aligned); the launcher sized the LDS for the largest slab
     const size_t gofs = ((sizeof(T) * ((size_t)nqi * k + nqi + 2 * (size_t)cap + TH) + 15) / 16) * 16;
     int4* Geo = reinterpret_cast<int4*>(smem + gofs);
+    // probe (mf_strata_set_probe): per position, in LDS during the launch
+    // (no global store on the step path): s_memrealtime when the apply
+    // cursor enters it, wave 0's spin time waiting for its range, the time
+    // of the drain + barrier publishing before it -- copied out at the end
+    uint32_t* Pr = A.probe ? reinterpret_cast<uint32_t*>(Geo + n_seq) : nullptr;
+    auto now = []() __attribute__((always_inline)) {
+        return (uint32_t)__builtin_amdgcn_s_memrealtime();
+    };
     if (threadIdx.x == 0)
         s_base = __hip_atomic_load(done + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const Hyper<T> h = hyper_regs(A.h);
     strata_stage_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
     for (int p = threadIdx.x; p < n_seq; p += TH) {
+        if (Pr) Pr[p] = Pr[n_seq + p] = Pr[2 * n_seq + p] = 0u;
         const int s = seq.s[p];
         const int64_t blk = (int64_t)s * B + w;
         const int64_t st0 = A.bstep[blk];
@@ -1074,15 +1083,13 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_stream(StrataArgs<T> 
                     Poll& Po, auto full) __attribute__((always_inline)) {
         constexpr bool FULL = decltype(full)::value;
         // (1) the poll issued two steps ago: next range released?
-        {
-            const int pv = rfl(Po.v);
-            if (!relN && Po.p == pA + 1 && pv >= base + pA + 2 - C) relN = true;
-        }
+        if (!relN && Po.p == pA + 1 && rfl(Po.v) >= base + pA + 2 - C) relN = true;
         // (2) the first gathers of position pA + 1 are issued this step: its
         // user range must be released (per wave)
         const bool enter = jA + 2 == gA.nv;
         if (enter && !relN) {
             const int tgt = base + pA + 2 - C;
+            const uint32_t ts0 = Pr ? now() : 0u;
             int64_t spins = 0;
             while (rfl(buf_ld<16, int>(drs, (uint32_t)gN.wd * 4u)) < tgt) {
                 if (++spins > kStrataSpinLimit ||
@@ -1094,27 +1101,36 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_stream(StrataArgs<T> 
                 __builtin_amdgcn_s_sleep(2);
             }
             relN = true;
+            if (Pr && threadIdx.x == 0) Pr[n_seq + pA + 1] = now() - ts0;
             // every load of handed-off bytes below is sc1 (no stale L1 line):
             // only keep the compiler from hoisting them above the poll
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         }
         // (3) loads, oldest first: staging of the next slice, the poll, the
         // rows of g+2, the triples of g+4
+        // (each only on the steps that need it: a vector-memory instruction
+        // costs the CU's address unit ~16+ cycles even with every lane
+        // dropped, and a position needs its slice once, not every step)
         if constexpr (BIAS) {
             const bool on = enter && pA + 1 < n_seq;
             Sn.on = on;
+            if (on) {
 #pragma unroll
-            for (int q = 0; q < KB; ++q) {
-                const int x = (int)threadIdx.x + q * TH;
-                const bool ok = on && x < gN.nus;
-                Sn.v[q] = buf_ld<16, T>(brs, ok ? (uint32_t)(gN.ulo + x) * (uint32_t)sizeof(T)
-                                              : kBufDrop);
+                for (int q = 0; q < KB; ++q) {
+                    const int x = (int)threadIdx.x + q * TH;
+                    Sn.v[q] = buf_ld<16, T>(brs, x < gN.nus ? (uint32_t)(gN.ulo + x) *
+                                                                 (uint32_t)sizeof(T)
+                                                           : kBufDrop);
+                }
             }
         }
         {
-            const bool need = !relN && pA + 1 < n_seq;
-            Pn.p = pA + 1;
-            Pn.v = buf_ld<16, int>(drs, need ? (uint32_t)gN.wd * 4u : kBufDrop);
+            // polled at the first two steps of a position (read two steps
+            // later); a range not seen released by then is waited for at
+            // the step that first gathers from it
+            const bool need = !relN && pA + 1 < n_seq && jA < 2;
+            Pn.p = need ? pA + 1 : -1;
+            if (need) Pn.v = buf_ld<16, int>(drs, (uint32_t)gN.wd * 4u);
         }
         unpack_gather(Tc, Rc, full);
         load_tri(4, Tn);
@@ -1175,21 +1191,23 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_stream(StrataArgs<T> 
             // at the first step of this one
             const bool wb = jA == 0 && pA >= 1 && pA < n_seq && A.upd_user;
             const int sb = ((pA + 1) & 1) * cap;           // = slice of pA - 1
+            if (wb) {
 #pragma unroll
-            for (int q2 = 0; q2 < KB; ++q2) {
-                const int x = (int)threadIdx.x + q2 * TH;
-                const T v = Bus[sb + (x < cap ? x : cap - 1)];
-                buf_st<16>(brs, (wb && x < gP.nus) ? (uint32_t)(gP.ulo + x) * (uint32_t)sizeof(T)
-                                                  : kBufDrop, v);
+                for (int q2 = 0; q2 < KB; ++q2) {
+                    const int x = (int)threadIdx.x + q2 * TH;
+                    const T v = Bus[sb + (x < cap ? x : cap - 1)];
+                    buf_st<16>(brs, x < gP.nus ? (uint32_t)(gP.ulo + x) * (uint32_t)sizeof(T)
+                                               : kBufDrop, v);
+                }
             }
-            // (6) the slice staged last step into the next position's LDS
-            // slice (a dummy entry when nothing was staged)
+            // (6) the slice staged last step into the next position's LDS slice
             const int nb = ((pA + 1) & 1) * cap;
+            if (Sp.on) {
 #pragma unroll
-            for (int q2 = 0; q2 < KB; ++q2) {
-                const int x = (int)threadIdx.x + q2 * TH;
-                T* dst = (Sp.on && x < cap) ? &Bus[nb + x] : &Dum[threadIdx.x];
-                *dst = Sp.v[q2];
+                for (int q2 = 0; q2 < KB; ++q2) {
+                    const int x = (int)threadIdx.x + q2 * TH;
+                    if (x < cap) Bus[nb + x] = Sp.v[q2];
+                }
             }
         }
         lds_barrier();
@@ -1197,8 +1215,10 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_stream(StrataArgs<T> 
         // stored before this point, its bias slice at step 0)
         if (jA == 1 && pA >= 1 && pA < n_seq && pA - 1 == nextsig) {
             nextsig += D;
+            const uint32_t td0 = Pr ? now() : 0u;
             __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0)
             __syncthreads();
+            if (Pr && threadIdx.x == 0) Pr[2 * n_seq + pA] = now() - td0;
             if (threadIdx.x == 0)
                 __hip_atomic_store(done + w, base + pA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1211,6 +1231,7 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_stream(StrataArgs<T> 
             gN = gNN;
             gNN = geo(pA + 2);
             relN = pA + 1 < C || pA + 1 >= n_seq;
+            if (Pr && threadIdx.x == 0 && pA < n_seq) Pr[pA] = now();
         }
     };
 
@@ -1237,6 +1258,7 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_stream(StrataArgs<T> 
                 Bus[x] = buf_ld<16, T>(brs, (uint32_t)(gA.ulo + x) * (uint32_t)sizeof(T));
     }
     lds_barrier();
+    if (Pr && threadIdx.x == 0 && n_seq > 0) Pr[0] = now();
     auto run = [&](auto full) __attribute__((always_inline)) {
         // copies by step mod 3 (no register with a load in flight is copied):
         // step s applies R[s%3], gathers rows of s+2 from T[(s+2)%3] into
@@ -1263,6 +1285,16 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_stream(StrataArgs<T> 
     __syncthreads();
     if (threadIdx.x == 0)
         __hip_atomic_store(done + w, base + n_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (Pr) {
+        const uint32_t tend = now();
+        for (int p = threadIdx.x; p < n_seq; p += TH) {
+            int64_t* o = A.probe + ((int64_t)p * B + w) * 4;
+            o[0] = Pr[p];
+            o[1] = Pr[n_seq + p];
+            o[2] = Pr[2 * n_seq + p];
+            o[3] = tend;
+        }
+    }
     if (A.Dq)
         strata_delta_slab<T, W, KERN, TH>(A, ilo, nqi, Qs, Bis);
     else
@@ -1498,7 +1530,8 @@ struct StrataRun {
             if constexpr (kDeep == 2 && V <= 2) {      // (rows of <= 2 vectors per lane)
                 if ((p.flags & MF_FLAG_STREAM) && deep && a.cls > 1 && p.B <= 256 &&
                     cap <= 4 * TH) {
-                    slds = strata_stream_lds_bytes<T>(p.max_items, cap, p.k, TH, p.n_seq);
+                    slds = strata_stream_lds_bytes<T>(p.max_items, cap, p.k, TH, p.n_seq) +
+                           (a.probe ? 12 * (size_t)p.n_seq : 0);
                     if (slds <= (size_t)kLdsLimit)
                         sfn = cap <= 2 * TH
                                   ? reinterpret_cast<const void*>(

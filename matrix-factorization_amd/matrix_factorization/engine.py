@@ -67,6 +67,21 @@ def resolve_device(device=None) -> torch.device:
     return dev
 
 
+_WARMED = set()
+
+
+def _warm_device(dev: torch.device) -> None:
+    """mf_warmup once per device and process: the runtime loads the library's
+    code object at the first launch of any of its kernels -- done here, while
+    an engine is built (fit() builds it on a worker thread beside the
+    initial draws), instead of inside the first training epoch."""
+    if dev.type != "cuda" or dev.index in _WARMED:
+        return
+    with torch.cuda.device(dev):
+        _lib.call("mf_warmup", _VOID(torch.cuda.current_stream(dev).cuda_stream))
+    _WARMED.add(dev.index)
+
+
 def _tp(t: Optional[torch.Tensor]):
     if t is None or t.numel() == 0:
         return None
@@ -539,6 +554,7 @@ class SGDEngine:
                  global_mean: float = 0.0, eval_order: bool = True,
                  check_ids: bool = True, device_triples=None):
         self.dev = resolve_device(device)
+        _warm_device(self.dev)
         self.dtype = canonical_dtype(dtype)
         self.tdt, self.ndt, self.dcode = DTYPES[self.dtype]
         self.kernel = kernel
@@ -796,8 +812,13 @@ class SGDEngine:
             for e, _, _ in regroups:
                 if e.strata.n_strata != plan.n_strata or e.strata.B != plan.B:
                     raise RuntimeError("a regrouped plan differs from the engine's in shape")
+                self._regroup_buffers(e)
             self._regroups = regroups
         self.strata = plan
+        # the persistent sweep's workspace (position counters, error word)
+        # now, not in the first epoch
+        if self.n:
+            self._ensure_strata_ws(plan.B, plan.n_strata)
         return plan
 
     # relabelled plans, "regroupings" (DESIGN.md section 3.1): K - 1 more
@@ -856,6 +877,7 @@ class SGDEngine:
                       check_ids=False, device_triples=(uj_d, ij_d, self.r))
         e.strata_persistent = self.strata_persistent
         e.strata_deep_pipe = self.strata_deep_pipe
+        e.strata_stream = self.strata_stream
         e.strata_regroup = 1
         e._regroup_of = j                 # never regroups itself (env included)
         e.prepare_strata(n_blocks=B, waves=waves,
@@ -1061,6 +1083,23 @@ class SGDEngine:
     # user rows two steps ahead in the persistent sweep (MF_FLAG_DEEP_PIPE):
     # None = by the plan, True / False forced; env MF_STRATA_DEEP=0/1 overrides
     strata_deep_pipe: Optional[bool] = None
+    # the stream form of the multi-class persistent sweep (MF_FLAG_STREAM:
+    # one software pipeline through all positions of a launch, DESIGN.md
+    # section 5 "stream"); None = the default, True / False forced; env
+    # MF_STRATA_STREAM=0/1 overrides.  Used where it applies: persistent,
+    # user-range classes C > 1, the depth-2 pipeline.
+    strata_stream: Optional[bool] = None
+    # on: C3 FP64 SGD 24.27 -> 20.10 ms, FP32 11.11 -> 10.32 ms on one box
+    # (profiles/r05/bench_c3_stream_r05e.json, ..._nostream_same_box_r05e.json)
+    STREAM_DEFAULT = True
+
+    def _stream(self) -> bool:
+        env = os.environ.get("MF_STRATA_STREAM")
+        if env in ("0", "1"):
+            return env == "1"
+        if self.strata_stream is not None:
+            return bool(self.strata_stream)
+        return self.STREAM_DEFAULT
 
     def _deep_pipe(self, pl) -> bool:
         """By the plan: on for plans of few busy slots per step (the 8-wave
@@ -1112,26 +1151,49 @@ class SGDEngine:
         e, pu, pi = self._regroups[j]
         e.global_mean, e.gamma = self.global_mean, self.gamma
         e.min_rating, e.max_rating = self.min_rating, self.max_rating
-        if e.P is None or e.P.shape != self.P.shape:
-            e.load_params(P=torch.zeros_like(self.P), Q=torch.zeros_like(self.Q),
-                          bu=None if self.bu is None else torch.zeros_like(self.bu),
-                          bi=None if self.bi is None else torch.zeros_like(self.bi))
-        e.P.index_copy_(0, pu, self.P)
-        e.Q.index_copy_(0, pi, self.Q)
-        if self.bu is not None:
-            e.bu.index_copy_(0, pu, self.bu)
-        if self.bi is not None:
-            e.bi.index_copy_(0, pi, self.bi)
+        self._regroup_buffers(e)
+        # into the plan's labelling (one launch: P, Q, b_u, b_i scattered by
+        # the user / item relabellings), the sweep there, and back (gathered)
+        self._permute(e, pu, pi, scatter=True)
         self._ensure_strata_ws(e.strata.B, len(seq))
         e._strata_ws = self._strata_ws           # shared counters and error word
         out = e.epoch_strata(seq, seed, lr, reg, update_user, update_item, timing, persistent)
-        torch.index_select(e.P, 0, pu, out=self.P)
-        torch.index_select(e.Q, 0, pi, out=self.Q)
-        if self.bu is not None:
-            torch.index_select(e.bu, 0, pu, out=self.bu)
-        if self.bi is not None:
-            torch.index_select(e.bi, 0, pi, out=self.bi)
+        self._permute(e, pu, pi, scatter=False)
         return out
+
+    def _regroup_buffers(self, e) -> None:
+        """Parameter storage of a relabelled plan's engine (allocated once,
+        when the plan is built: an allocation inside the first regrouped
+        epoch cost ~20 ms of fit()'s epoch 2)."""
+        if self.P is None:
+            shapes = ((self.n_users, self.k), (self.n_items, self.k), (self.n_users,),
+                      (self.n_items,))
+            ref = [torch.empty(sh, dtype=self.tdt, device=self.dev) for sh in shapes]
+            if self.bias_only:
+                ref[0] = ref[1] = None
+        else:
+            ref = [self.P, self.Q, self.bu, self.bi]
+        have = (e.P, e.Q, e.bu, e.bi)
+        if all((a is None) == (b is None) and (a is None or a.shape == b.shape)
+               for a, b in zip(have, ref)):
+            return
+        e.load_params(*(None if t is None else torch.zeros_like(t) for t in ref))
+
+    def _permute(self, e, pu, pi, scatter: bool) -> None:
+        """mf_permute_rows: scatter (this engine's parameters -> the plan's
+        labelling: e.X[p[x]] = X[x]) or gather (back: X[x] = e.X[p[x]])."""
+        jobs = [(e.P, self.P, pu), (e.Q, self.Q, pi), (e.bu, self.bu, pu), (e.bi, self.bi, pi)]
+        jobs = [(a, b, p) for a, b, p in jobs if a is not None and b is not None]
+        n = len(jobs)
+        dst = (ctypes.c_void_p * n)(*[(a if scatter else b).data_ptr() for a, b, _ in jobs])
+        src = (ctypes.c_void_p * n)(*[(b if scatter else a).data_ptr() for a, b, _ in jobs])
+        idx = (ctypes.c_void_p * n)(*[p.data_ptr() for _, _, p in jobs])
+        rows = (ctypes.c_int64 * n)(*[b.shape[0] for _, b, _ in jobs])
+        rb = (ctypes.c_int32 * n)(*[b[0].numel() * b.element_size() if b.shape[0] else 4
+                                    for _, b, _ in jobs])
+        with torch.cuda.device(self.dev):
+            _lib.call("mf_permute_rows", n, dst, src, idx, rows, rb, 0 if not scatter else 1,
+                      self.stream)
 
     def _ensure_strata_ws(self, B: int, n_seq: int) -> None:
         wsb = int(_lib.load().mf_strata_workspace_bytes(B, n_seq))
@@ -1152,6 +1214,8 @@ class SGDEngine:
         flags = _lib.MF_FLAG_PERSISTENT if persistent else 0
         if persistent and self._deep_pipe(pl):
             flags |= _lib.MF_FLAG_DEEP_PIPE
+            if pl.classes > 1 and self._stream():
+                flags |= _lib.MF_FLAG_STREAM
         if os.environ.get("MF_STRATA_COOP") == "0" or _under_rocprofiler():
             flags |= _lib.MF_FLAG_NO_COOP
         if os.environ.get("MF_STRATA_EARLY") == "0":

@@ -566,3 +566,61 @@ def test_regrouped_plans(dtype, phases, K):
     finally:
         del os.environ["MF_STRATA_REGROUP"]
     assert len(e4._regroups) == 2 and all(not e._regroups for e, _, _ in e4._regroups)
+
+
+@pytest.mark.parametrize("dtype,kernel,k,B,C,waves,phases,nu,ni,nnz", [
+    ("float64", "linear", 64, 4, 2, None, None, 3000, 900, 120000),
+    ("float32", "linear", 64, 16, 4, 8, None, 3000, 900, 120000),
+    ("float32", "sigmoid", 32, 8, 2, 8, None, 3000, 900, 120000),
+    ("float64", "rbf", 16, 5, 3, None, None, 3000, 900, 120000),
+    ("float64", "linear", 64, 4, 2, None, 2, 3000, 900, 120000),   # item phases
+    ("float32", "linear", 64, 16, 4, 8, None, 4000, 1500, 3000),   # empty / 1-3 step blocks
+    ("float64", "sigmoid", 32, 6, 4, None, None, 5000, 600, 60000),
+])
+def test_stream_equals_per_stratum_launches(dtype, kernel, k, B, C, waves, phases, nu, ni, nnz,
+                                            monkeypatch):
+    """The stream form of the multi-class persistent sweep (MF_FLAG_STREAM:
+    one software pipeline through every position of the launch, the next
+    block's triples and rows loaded while the current block's last steps
+    apply, the bias slices double-buffered) applies the same sequential order:
+    bit-identical to one launch per stratum over 3 epochs, and the oracle's
+    sweep in plan.serial_order -- blocks of every length, empty ones and ones
+    shorter than the 4-step lookahead included."""
+    import oracle
+    from matrix_factorization.engine import stratum_order
+
+    monkeypatch.setenv("MF_STRATA_DEEP", "1")
+    u, i, r = _synthetic(95, nu, ni, nnz)
+    rs = np.random.RandomState(96)
+    P0 = rs.normal(0, 0.1, (nu, k)); Q0 = rs.normal(0, 0.1, (ni, k))
+    bu0 = rs.normal(0, 0.1, nu); bi0 = rs.normal(0, 0.1, ni)
+    out = []
+    n_ph = phases or 1
+    for stream in (True, False):
+        monkeypatch.setenv("MF_STRATA_STREAM", "1" if stream else "0")
+        eng = _engine(u, i, r, nu, ni, k, kernel, dtype, P0, Q0, bu0, bi0)
+        eng.strata_regroup = 1
+        plan = eng.prepare_strata(n_blocks=B, waves=waves, phases=phases, classes=C)
+        eps = []
+        for ep in range(3):
+            seq = stratum_order(np.random.RandomState(ep), plan)
+            ms = eng.epoch_strata(seq, 6000 + ep, lr=0.01, reg=0.02, persistent=stream,
+                                  timing=True)
+            assert ms[1] == (n_ph if stream else n_ph * C * B)
+            eps.append((seq, 6000 + ep))
+        eng.check_strata()
+        out.append(eng.params_numpy())
+    if nnz < 10000:
+        steps = np.diff(plan.bstep) if hasattr(plan, "bstep") else None
+        assert steps is None or (steps.min() == 0 and (steps < 4).mean() > 0.5)
+    for a, b in zip(*out):
+        assert np.array_equal(a, b)
+    hyp = dict(kernel=kernel, gamma=1.0 / k, min_rating=1.0, max_rating=5.0)
+    P2, Q2, bu2, bi2 = P0.copy(), Q0.copy(), bu0.copy(), bi0.copy()
+    for seq, seed in eps:
+        order = eng.serial_order(seq, seed)
+        oracle.sgd_pass(eng.u_host, eng.i_host, eng.r_host.astype(np.float64), eng.global_mean,
+                        bu2, bi2, P2, Q2, lr=0.01, reg=0.02, order=order, **hyp)
+    tol = 1e-11 if dtype == "float64" else 1e-4
+    for g, o in zip(out[0], (P2, Q2, bu2, bi2)):
+        _close(g, o, tol)

@@ -136,7 +136,7 @@ def main():
         t0 = time.time()
         e = fresh()
         np.random.seed(s)
-        order = np.arange(nnz, dtype=np.int64)
+        order = np.arange(nnz, dtype=np.int32)     # (32-bit: the chunked level builder)
         for ep in range(E):
             _prep.legacy_shuffle_(order)           # = np.random.shuffle(order), :371
             e.epoch_exact(order, args.lr, args.reg)
