@@ -1121,8 +1121,10 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
             launches = launches_per_epoch * len(events)
             alg = alg_epoch * len(events)                           # algorithmic bytes
             achieved = alg / sgd_s / 1e9
-            kname = (("k_sgd_strata_epoch" if persistent else "k_sgd_strata") if strata
-                     else "k_sgd_batch")
+            stream = (strata and persistent and cls > 1 and eng._deep_pipe(plan)
+                      and eng._stream())
+            kname = ((("k_sgd_strata_stream" if stream else "k_sgd_strata_epoch")
+                      if persistent else "k_sgd_strata") if strata else "k_sgd_batch")
             traffic = traffic_from_profiles(args.workload, world, args.schedule
                                             + ("_persistent" if persistent else ""),
                                             args.dtype, kname, emulate=emu)

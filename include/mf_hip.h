@@ -91,6 +91,11 @@ enum {
                                  while the current block's last steps apply,
                                  the bias slices double-buffered in LDS); the
                                  same sequential order, bit for bit */
+    MF_FLAG_PREPARE = 2048,   /* mf_sgd_epoch_strata: no launch -- only the
+                                 launcher's one-time runtime work for this plan
+                                 (kernel attributes, the co-residency query),
+                                 so the first epoch does not pay it; the
+                                 parameter pointers are not touched */
     /* mf_sgd_epoch_strata: bits 24..27 = C - 1, the plan's user-range classes
        (mf_strata_plan_build_classes; 0 = C = 1, the plain B x B plan) */
     MF_FLAG_CLASSES_SHIFT = 24

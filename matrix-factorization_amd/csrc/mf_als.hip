@@ -830,6 +830,8 @@ int als_go(const AlsArgs& a, int32_t n, hipStream_t stream) {
     return MF_OK;
 }
 
+void touch_als(hipStream_t s) { hipLaunchKernelGGL(k_touch<7>, dim3(1), dim3(64), 0, s); }
+
 }  // namespace mf
 
 using namespace mf;

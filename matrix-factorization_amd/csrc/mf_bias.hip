@@ -382,6 +382,8 @@ __global__ __launch_bounds__(kBlock) void k_permute_rows(PermJobs J) {
     else if (rb % 8 == 0 && al % 8 == 0) permute_job<uint2>(J, j, t0, stride);
     else permute_job<uint32_t>(J, j, t0, stride);
 }
+void touch_bias(hipStream_t s) { hipLaunchKernelGGL(k_touch<5>, dim3(1), dim3(64), 0, s); }
+
 }  // namespace mf
 
 extern "C" int mf_permute_rows(int32_t n_jobs, void* const* dst, const void* const* src,

@@ -10,6 +10,9 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <stdint.h>
 
 #include "../../include/mf_hip.h"
@@ -173,5 +176,36 @@ inline int kpad_of(int k) {
     while (kp < k) kp <<= 1;
     return kp;
 }
+
+// MF_LAUNCH_TRACE=1: host time of the launcher's runtime calls on stderr
+// (diagnostic: where a first epoch's host time goes)
+struct LaunchTrace {
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    static bool on() {
+        static const bool v = std::getenv("MF_LAUNCH_TRACE") != nullptr;
+        return v;
+    }
+    void mark(const char* what) const {
+        if (!on()) return;
+        const double ms = std::chrono::duration<double, std::milli>(
+                              std::chrono::steady_clock::now() - t0).count();
+        std::fprintf(stderr, "[mf launch] %-24s %9.3f ms\n", what, ms);
+    }
+};
+
+// One empty kernel per translation unit (U: the unit's number).  HIP loads a
+// unit's code object at the first launch of one of its kernels -- ~6-10 ms
+// for the large units (MF_LAUNCH_TRACE, profiles/r05) -- so mf_warmup
+// launches every unit's k_touch<U> once per device up front, and an engine's
+// first epoch does not pay it.
+template <int U>
+__global__ void k_touch() {}
+void touch_rows_f32(hipStream_t s);
+void touch_rows_f64(hipStream_t s);
+void touch_strata_f32(hipStream_t s);
+void touch_strata_f64(hipStream_t s);
+void touch_bias(hipStream_t s);
+void touch_topk(hipStream_t s);
+void touch_als(hipStream_t s);
 
 }  // namespace mf

@@ -1270,6 +1270,7 @@ struct SseRun {
         static int resident_tab[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // per instantiation and variant
         int& resident = resident_tab[var];
         if (resident == 0) {
+            const LaunchTrace lt;
             int dev = 0, cus = 0, per_cu = 0;
             if (hipGetDevice(&dev) == hipSuccess &&
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) ==
@@ -1279,6 +1280,7 @@ struct SseRun {
                 resident = cus * per_cu;
             else
                 resident = kSseMaxBlocks;
+            lt.mark("sse occupancy");
         }
         constexpr int64_t kSseRatingsPerWave = 6144;
         const int64_t by_size = p.n / (kSseRatingsPerWave * kWavesPerBlock);
@@ -1291,9 +1293,11 @@ struct SseRun {
         }
         if (p.max_blocks > 0) blocks = std::min(blocks, p.max_blocks);
         blocks = std::max(p.S.n, (blocks / p.S.n) * p.S.n);
+        const LaunchTrace lt2;
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(kBlock), 0, p.stream, a, p.S);
         hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(kBlock), 0, p.stream,
                            (const double*)p.partials, blocks, p.sse_out);
+        lt2.mark("sse launches");
         MF_HIP_CHECK(hipGetLastError());
         return MF_OK;
     }

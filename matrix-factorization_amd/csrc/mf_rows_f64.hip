@@ -15,4 +15,6 @@ int sse_launch_f64(const SseParams& p) {
 }
 
 
+void touch_rows_f64(hipStream_t s) { hipLaunchKernelGGL(k_touch<2>, dim3(1), dim3(64), 0, s); }
+
 }  // namespace mf

@@ -289,7 +289,27 @@ extern "C" size_t mf_strata_workspace_bytes(int32_t n_blocks, int32_t n_seq) {
 __global__ void k_warmup() {}
 
 extern "C" int mf_warmup(void* stream) {
-    hipLaunchKernelGGL(k_warmup, dim3(1), dim3(64), 0, (hipStream_t)stream);
+    const hipStream_t s = (hipStream_t)stream;
+    const LaunchTrace lt;
+    hipLaunchKernelGGL(k_warmup, dim3(1), dim3(64), 0, s);
+    lt.mark("warmup: sgd unit");
+    touch_rows_f32(s);
+    touch_rows_f64(s);
+    lt.mark("warmup: rows units");
+    touch_strata_f32(s);
+    touch_strata_f64(s);
+    lt.mark("warmup: strata units");
+    touch_bias(s);
+    touch_topk(s);
+    touch_als(s);
+    lt.mark("warmup: other units");
+    {   // the cooperative launch path (persistent sweeps)
+        void* no_args[1] = {nullptr};
+        (void)hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_warmup), dim3(1),
+                                         dim3(64), no_args, 0u, s);
+        (void)hipGetLastError();
+    }
+    lt.mark("warmup: cooperative");
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MF_OK : hip_fail(e, "mf_warmup");
 }
@@ -372,7 +392,8 @@ static int strata_epoch(const int32_t* user_ids, const int32_t* item_ids,
             return MF_ERR_INVALID;
         }
     }
-    if (!user_features || !item_features || (kernel != MF_RBF && (!user_biases || !item_biases))) {
+    if (!(flags & MF_FLAG_PREPARE) &&
+        (!user_features || !item_features || (kernel != MF_RBF && (!user_biases || !item_biases)))) {
         set_error("NULL parameter array");
         return MF_ERR_INVALID;
     }

@@ -946,8 +946,7 @@ __global__ __launch_bounds__(NW * kWave) void k_sgd_strata_stream(StrataArgs<T> 
     const int kv = k / W;
     T* Qs = reinterpret_cast<T*>(smem);
     T* Bis = Qs + (size_t)nqi * k;
-    T* Bus = Bis + nqi;                  // two slices of `cap`
-    T* Dum = Bus + 2 * (size_t)cap;      // one dummy entry per thread
+    T* Bus = Bis + nqi;                  // two slices of `cap`, then one dummy entry per thread
     // the geometry table follows this workgroup's slab and slices (16-B
     // aligned); the launcher sized the LDS for the largest slab
     const size_t gofs = ((sizeof(T) * ((size_t)nqi * k + nqi + 2 * (size_t)cap + TH) + 15) / 16) * 16;
@@ -1501,7 +1500,7 @@ struct StrataRun {
         a.xtab = nullptr;
         a.early = (p.flags & MF_FLAG_NO_EARLY_POLL) ? 0 : 1;
         hipEvent_t ev[2] = {nullptr, nullptr};
-        if (p.kernel_ms) {
+        if (p.kernel_ms && !(p.flags & MF_FLAG_PREPARE)) {
             MF_HIP_CHECK(hipEventCreate(&ev[0]));
             MF_HIP_CHECK(hipEventCreate(&ev[1]));
             MF_HIP_CHECK(hipEventRecord(ev[0], p.stream));
@@ -1540,14 +1539,19 @@ struct StrataRun {
                                         k_sgd_strata_stream<T, W, GS, V, KERN, S, NW, 4>);
                 }
             }
+            const LaunchTrace lt0;
             if (sfn) {
                 MF_HIP_CHECK(hipFuncSetAttribute(sfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                  (int)slds));
+                lt0.mark("hipFuncSetAttribute");
                 persistent = strata_coresident(sfn, p.B, slds, TH);
             } else {
                 persistent = strata_coresident(reinterpret_cast<const void*>(efn), p.B, lds, TH);
             }
+            lt0.mark("strata_coresident");
+            if (p.flags & MF_FLAG_PREPARE) return MF_OK;       // attributes / occupancy only
             if (persistent) {
+                const LaunchTrace lt1;
                 int32_t* done = static_cast<int32_t*>(p.ws);
                 int32_t* err = done + p.B;
                 // the (otherwise unused) tail of the workspace holds the XCC
@@ -1579,6 +1583,7 @@ struct StrataRun {
                         (void)hipGetLastError();
                         persistent = false;
                     }
+                    lt1.mark("stream launch");
                 } else if (p.flags & MF_FLAG_NO_COOP) {
                     hipLaunchKernelGGL(efn, dim3((unsigned)p.B), dim3(TH), lds,
                                        p.stream, a, sq, nseq, done, err);
@@ -1597,6 +1602,7 @@ struct StrataRun {
                 }
             }
         }
+        if (p.flags & MF_FLAG_PREPARE) return MF_OK;
         if (!persistent) {
             const int64_t nq = p.n_items * (int64_t)p.k;
             if (p.dq) {   // delta-out: keep the start values in D (see k_delta_swap)

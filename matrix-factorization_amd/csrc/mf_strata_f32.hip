@@ -10,4 +10,6 @@ int strata_launch_f32(const StrataParams& p) {
     return dispatch_rows<float>(p.k, p.kernel, r);
 }
 
+void touch_strata_f32(hipStream_t s) { hipLaunchKernelGGL(k_touch<3>, dim3(1), dim3(64), 0, s); }
+
 }  // namespace mf

@@ -10,4 +10,6 @@ int strata_launch_f64(const StrataParams& p) {
     return dispatch_rows<double>(p.k, p.kernel, r);
 }
 
+void touch_strata_f64(hipStream_t s) { hipLaunchKernelGGL(k_touch<4>, dim3(1), dim3(64), 0, s); }
+
 }  // namespace mf

@@ -20,6 +20,7 @@
 namespace mf {
 
 constexpr int kTopkMaxAmount = 2048;
+using bf16x8 = __attribute__((ext_vector_type(8))) __bf16;
 constexpr int kTopkItemsPerWave = 256;
 
 __device__ __forceinline__ uint64_t order_key(double s) {
@@ -526,13 +527,34 @@ struct MmArgs {
     int32_t* overflow;
     int32_t defer;                       // light users skip the exclusion search until the end
     int32_t fill;                        // k_topk_mw: compact a list past this many entries
+    const int32_t* probe;                // k_topk_mw: probe items (k_topk_probe), n_probe of them
+    int32_t n_probe, probe_group;        // ... one per group of probe_group consecutive ids
+    const bf16x8* Qs;                    // k_topk_mw<.., BF>: Q split into bf16 hi + lo (k_topk_split_q)
 };
 
-// max item-row norm and max |b_i| (non-negative floats: integer max of the bits)
+// max item-row norm and max |b_i| (non-negative floats: integer max of the bits);
+// the blocks past the items': max query-user row norm into stats[2]
 __global__ __launch_bounds__(kBlock) void k_topk_mm_stats(const float* __restrict__ Q,
                                                           const float* __restrict__ Bi,
                                                           int32_t n_items, int32_t k,
-                                                          float* stats) {
+                                                          float* stats,
+                                                          const int32_t* __restrict__ users,
+                                                          int32_t nq_users,
+                                                          const float* __restrict__ P) {
+    const int64_t nb_items = ((int64_t)n_items + kBlock - 1) / kBlock;
+    if ((int64_t)blockIdx.x >= nb_items) {
+        const int64_t q = ((int64_t)blockIdx.x - nb_items) * kBlock + threadIdx.x;
+        float pn = 0.f;
+        const int32_t uu = q < nq_users ? users[q] : -1;
+        if (uu >= 0) {
+            const float* pr = P + (int64_t)uu * k;
+            for (int f = 0; f < k; ++f) pn = __builtin_fmaf(pr[f], pr[f], pn);
+            pn = sqrtf(pn);
+        }
+        for (int o = 32; o > 0; o >>= 1) pn = fmaxf(pn, __shfl_xor(pn, o, kWave));
+        if ((threadIdx.x & (kWave - 1)) == 0) atomicMax(reinterpret_cast<int*>(stats) + 2, __float_as_int(pn));
+        return;
+    }
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     float nq = 0.f, nb = 0.f;
     if (i < n_items) {
@@ -551,6 +573,70 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm_stats(const float* __restric
         atomicMax(reinterpret_cast<int*>(stats), __float_as_int(nq));
         atomicMax(reinterpret_cast<int*>(stats) + 1, __float_as_int(nb));
     }
+}
+
+// k_topk_probe: the probe items of k_topk_mw -- one per group of G consecutive
+// item ids, the group's best by b_i + rho ||q_i|| (rho = half the largest
+// query-user norm, stats[2]; ties to the lower id), one wave per group.  Any
+// set of items gives a valid admission floor (k_topk_mw); this one is meant
+// to hold items that rank high for many users, so that the floor is high.
+// Ascending ids (group order), one item per group: excluded ones are found
+// by id / G.
+__global__ __launch_bounds__(kBlock) void k_topk_probe(const float* __restrict__ Q,
+                                                       const float* __restrict__ Bi,
+                                                       int32_t n_items, int32_t k, int32_t G,
+                                                       int32_t n_probe,
+                                                       const float* __restrict__ stats,
+                                                       int32_t* __restrict__ probe) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int g = blockIdx.x * kWavesPerBlock + (int)threadIdx.x / kWave;
+    if (g >= n_probe) return;                            // wave-uniform
+    const float rho = 0.5f * stats[2];
+    const int64_t lo = (int64_t)g * G, hi = min((int64_t)n_items, lo + G);   // lo < n_items (caller)
+    float best = -INFINITY;
+    int32_t bid = 0x7fffffff;
+    for (int64_t it = lo + lane; it < hi; it += kWave) {
+        const float* q = Q + it * k;
+        float nn = 0.f;
+        for (int f = 0; f < k; f += 4) {
+            const float4 v = *reinterpret_cast<const float4*>(q + f);
+            nn = __builtin_fmaf(v.x, v.x, nn); nn = __builtin_fmaf(v.y, v.y, nn);
+            nn = __builtin_fmaf(v.z, v.z, nn); nn = __builtin_fmaf(v.w, v.w, nn);
+        }
+        const float key = Bi[it] + rho * sqrtf(nn);
+        if (key > best) { best = key; bid = (int32_t)it; }   // ascending: first of equals
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o, kWave);
+        const int32_t oi = __shfl_xor(bid, o, kWave);
+        if (ob > best || (ob == best && oi < bid)) { best = ob; bid = oi; }
+    }
+    if (lane == 0) probe[g] = bid == 0x7fffffff ? (int32_t)lo : bid;   // (NaN keys: the first)
+}
+
+// k_topk_split_q: the item rows as k_topk_mw<.., BF> reads them -- item x,
+// lane half h: NB groups of 8 hi parts, then their NB lo parts (x = hi + lo
+// + e, hi = bf16(x), lo = bf16(x - hi)); group s, element j = column
+// h seg + 8 s + j (zero past seg or k).  One thread per (item, half, group).
+__global__ __launch_bounds__(kBlock) void k_topk_split_q(const float* __restrict__ Q,
+                                                         int32_t n_items, int32_t k, int32_t seg,
+                                                         int32_t nb, bf16x8* __restrict__ Qs) {
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= (int64_t)n_items * 2 * nb) return;
+    const int64_t it = t / (2 * nb);
+    const int rem = (int)(t - it * 2 * nb), h = rem / nb, g = rem % nb;
+    bf16x8 hi, lo;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int ci = 8 * g + j, col = h * seg + ci;
+        const float x = ci < seg && col < k ? Q[it * k + col] : 0.f;
+        const __bf16 xh = (__bf16)x;
+        hi[j] = xh;
+        lo[j] = (__bf16)(x - (float)xh);
+    }
+    bf16x8* o = Qs + (it * 2 + h) * 2 * nb;
+    o[g] = hi;
+    o[nb + g] = lo;
 }
 
 // (score desc, id asc) bitonic sort of n (power of two) float-keyed entries
@@ -934,6 +1020,9 @@ constexpr int kMwCap = kWave;            // one entry per lane in a compaction
 constexpr int kMwMaxAmount = 16;         // amount + band must fit kMwCap - 32 after a compaction
 constexpr int kMwUsers = 32 * kWavesPerBlock;
 constexpr int kMwExCap = 768;            // excluded ids of a wave's users in its split, cached in LDS
+constexpr int kMwProbe = 512;            // probe items (k_topk_probe) at most
+constexpr int kMwProbeWords = kMwProbe / 64;
+static_assert(32 * kMwProbeWords * 8 <= kMwExCap * 4, "probe bits share the exclusion cache");
 
 // v[l] = x (x and l wave-uniform), the other lanes keep v
 __device__ __forceinline__ int writelane_i(int x, int l, int v) {
@@ -942,20 +1031,29 @@ __device__ __forceinline__ int writelane_i(int x, int l, int v) {
 __device__ __forceinline__ float readlane_f(float v, int j) {
     return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), j));
 }
+__device__ __forceinline__ float writelane_f(float x, int l, float v) {
+    return __builtin_bit_cast(float, writelane_i(__builtin_bit_cast(int, x), l,
+                                                 __builtin_bit_cast(int, v)));
+}
 
-template <int SEG, bool PIPE = true>
+template <int SEG, bool PIPE = true, bool BF = false>
 __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
     constexpr int CAP = kMwCap;
+    constexpr int NB = (SEG + 7) / 8;                    // BF: bf16 MFMAs per term and tile
     using f32x16 = __attribute__((ext_vector_type(16))) float;
     __shared__ float s_sc[kMwUsers][CAP];
     __shared__ int32_t s_id[kMwUsers][CAP];
     __shared__ float s_m[kMwUsers];
     __shared__ int64_t s_elo[kMwUsers], s_ehi[kMwUsers];
-    __shared__ int32_t s_ex[kWavesPerBlock][kMwExCap];   // per wave: its users' ids, packed
-    __shared__ int s_exoff[kMwUsers];                      // offset in s_ex[wave], -1: not cached
+    // per wave: its users' excluded ids of the split, packed (after the probe
+    // walk); during it, the users' probe-exclusion bits
+    __shared__ __align__(16) int32_t s_un[kWavesPerBlock * kMwExCap];
+    __shared__ int s_exoff[kMwUsers];                      // offset in the wave's cache, -1: not cached
     __shared__ int s_lost;
     const int tid = threadIdx.x, lane = tid & (kWave - 1), wv = tid / kWave;
     const int c = lane & 31, h = lane >> 5;
+    int32_t* const s_exw = s_un + wv * kMwExCap;
+    uint64_t* const s_pexw = reinterpret_cast<uint64_t*>(s_exw);
     const int split = blockIdx.x;
     const int m0 = 32 * wv;                              // this wave's users: m0 .. m0 + 31
     const int q0 = blockIdx.y * kMwUsers + m0;
@@ -964,13 +1062,22 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
     const int ibeg = (int)min((int64_t)A.n_items, span * split);
     const int iend = (int)min((int64_t)A.n_items, span * (split + 1));
     const float qmax = A.stats[0], bimax = A.stats[1];
-    const float ck = 2.f * (float)(k + 8) * 0x1p-24f;
+    // |s' - s| <= ck ||p|| max ||q|| (+ the bias additions, below), doubled:
+    // f32 MFMA: both orders within gamma_(k+8) sum |p_i q_i|.  BF (3-term
+    // bf16 split, p = ph + pl + ep with |ep| <= 2^-14 |p| even for truncating
+    // conversions): the dropped terms ph eq + pl ql + ep q within 3 2^-14
+    // sum |p_i q_i|, the MFMA's sums of 3k exact products and k_read's tree
+    // within (4k + 8) 2^-23 (faithful rounding, either direction)
+    const float ck = BF ? 2.02f * (3.f * 0x1p-14f + (float)(4 * k + 8) * 0x1p-23f)
+                        : 2.f * (float)(k + 8) * 0x1p-24f;
     if (tid == 0) s_lost = 0;
     float bu_own = 0.f;
     int ex_n = 0;                                        // lane r < 32: excluded ids of user r in the split
     // lane r < 32: count and admission bound of user m0 + r (no query: never admits)
     int lcnt = 0;
     float ladm = q0 + c < A.nq ? -INFINITY : INFINITY;
+    float lfloor = -INFINITY;                            // lane r < 32: user r's floor (probe walk)
+    bool probing = false;
     if (lane < 32) {
         const int qy = q0 + lane;
         const int32_t uu = qy < A.nq ? A.users[qy] : -1;
@@ -993,41 +1100,10 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
         s_ehi[m0 + lane] = hi;
         ex_n = (int)(hi - lo);
     }
-    // The excluded ids of this wave's users in the split, packed into the
-    // wave's LDS area (users in order while they fit; the rest search HBM):
-    // a compaction then checks its list without a global-memory round trip.
-    {
-        int incl = ex_n;                                 // inclusive scan over lanes 0..31
-        for (int o = 1; o < 32; o <<= 1) {
-            const int t = __shfl_up(incl, o, kWave);
-            if (c >= o) incl += t;
-        }
-        const int off = incl - ex_n;
-        const bool fits = incl <= kMwExCap;
-        if (lane < 32) s_exoff[m0 + lane] = fits ? off : -1;
-        const uint64_t fm = __builtin_amdgcn_ballot_w64(lane < 32 && fits);
-        const int nfit = __popcll(fm);                   // users 0 .. nfit-1 are cached
-        const int ntot = nfit > 0 ? __builtin_amdgcn_readlane(incl, nfit - 1) : 0;
-        asm volatile("" ::: "memory");
-        // all loads in flight first, then the LDS stores
-        constexpr int kSteps = kMwExCap / kWave;
-        int32_t val[kSteps];
-#pragma unroll
-        for (int j = 0; j < kSteps; ++j) {
-            const int t = lane + kWave * j;
-            val[j] = 0;
-            if (t < ntot) {
-                int u = 0;                               // last user whose range starts at or before t
-                for (int r = 1; r < nfit; ++r) u += __builtin_amdgcn_readlane(off, r) <= t ? 1 : 0;
-                val[j] = A.ex_items[s_elo[m0 + u] + (t - s_exoff[m0 + u])];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < kSteps; ++j)
-            if (lane + kWave * j < ntot) s_ex[wv][lane + kWave * j] = val[j];
-    }
     // A operands: lane (c, h) holds user q0 + c, columns h SEG .. h SEG + SEG-1
+    // (BF: as bf16 hi + lo, element j of MFMA s = column h SEG + 8 s + j)
     float a[SEG];
+    bf16x8 ah[NB], al[NB];
     {
         const int qy = q0 + c;
         const int32_t uu = qy < A.nq ? A.users[qy] : -1;
@@ -1040,6 +1116,17 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
             a[j + 0] = ok ? v.x : 0.f; a[j + 1] = ok ? v.y : 0.f;
             a[j + 2] = ok ? v.z : 0.f; a[j + 3] = ok ? v.w : 0.f;
         }
+        if constexpr (BF) {
+#pragma unroll
+            for (int s2 = 0; s2 < NB; ++s2)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float x = 8 * s2 + j < SEG ? a[8 * s2 + j] : 0.f;
+                    const __bf16 xh = (__bf16)x;
+                    ah[s2][j] = xh;
+                    al[s2][j] = (__bf16)(x - (float)xh);
+                }
+        }
     }
     // accumulator row i of lane (c, h) is user r(i, h) = (i & 3) + 8 (i >> 2) + 4 h
     float ubu[16], uadm[16];
@@ -1051,26 +1138,54 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
         uadm[i] = q0 + r < A.nq && A.defer != 2 ? -INFINITY : INFINITY;
     }
     __syncthreads();                                     // the setup's LDS words
-    auto load_b = [&](int it0, float (&b)[SEG], float& bi) __attribute__((always_inline)) {
-        const int n = it0 + c;
-        const int nn = n < iend ? n : (ibeg < iend ? ibeg : 0);   // empty split: row 0
-        const float* qr = A.Q + (int64_t)nn * k;
-        bi = A.Bi[nn];
+    float b[SEG], bi;
+    bf16x8 bh[NB], bl[NB];
+    // B operands (and b_i) of item nn: part 0 / 1 = those the first / second
+    // half of a tile's MFMAs read (the MFMAs of rows 0..7 / 8..15 in the
+    // pipelined loop), 2 = all
+    auto fetch = [&](int nn, int part) __attribute__((always_inline)) {
+        if (part != 1) bi = A.Bi[nn];
+        if constexpr (BF) {
+            const bf16x8* qs = A.Qs + ((int64_t)nn * 2 + h) * 2 * NB;
+            constexpr int HB = NB / 2;
 #pragma unroll
-        for (int j = 0; j < SEG; j += 4) {
-            const int c0 = h * SEG + j;
-            const float4 v = *reinterpret_cast<const float4*>(qr + (c0 < k ? c0 : 0));
-            b[j + 0] = v.x; b[j + 1] = v.y; b[j + 2] = v.z; b[j + 3] = v.w;
+            for (int s2 = part == 1 ? HB : 0; s2 < (part == 0 ? HB : NB); ++s2) {
+                bh[s2] = qs[s2];
+                bl[s2] = qs[NB + s2];
+            }
+        } else {
+            const float* qr = A.Q + (int64_t)nn * k;
+            constexpr int H4 = (SEG / 2) & ~3;
+#pragma unroll
+            for (int j = part == 1 ? H4 : 0; j < (part == 0 ? H4 : SEG); j += 4) {
+                const int c0 = h * SEG + j;
+                const float4 v = *reinterpret_cast<const float4*>(qr + (c0 < k ? c0 : 0));
+                b[j + 0] = v.x; b[j + 1] = v.y; b[j + 2] = v.z; b[j + 3] = v.w;
+            }
         }
     };
-    float b[SEG], bi;
-    load_b(ibeg, b, bi);
+    auto item_of = [&](int it0) __attribute__((always_inline)) -> int {
+        const int n = it0 + c;
+        return n < iend ? n : (ibeg < iend ? ibeg : 0);  // empty split: row 0
+    };
+    auto load_b = [&](int it0) __attribute__((always_inline)) { fetch(item_of(it0), 2); };
+    // the NM MFMAs of a tile; mfma_m issues the m-th (BF: for each 16 columns
+    // lo x hi, hi x lo, hi x hi)
+    constexpr int NM = BF ? 3 * NB : SEG;
+    auto mfma_m = [&](f32x16& x, int m) __attribute__((always_inline)) {
+        if constexpr (BF) {
+            const int s2 = m / 3, t = m % 3;
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t == 0 ? al[s2] : ah[s2],
+                                                        t == 1 ? bl[s2] : bh[s2], x, 0, 0, 0);
+        } else {
+            x = __builtin_amdgcn_mfma_f32_32x32x2f32(a[m], b[m], x, 0, 0, 0);
+        }
+    };
     auto tile = [&](f32x16& x) __attribute__((always_inline)) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) x[i] = 0.f;
 #pragma unroll
-        for (int s = 0; s < SEG; ++s)
-            x = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], x, 0, 0, 0);
+        for (int m = 0; m < NM; ++m) mfma_m(x, m);
     };
     // the per-row admission ballots of a tile (row i: users r(i, 0) in the
     // low half, r(i, 1) in the high half), kept for insert
@@ -1100,13 +1215,13 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
         if (lane < n) { v = s_sc[m][lane]; it = s_id[m][lane]; }
         const int64_t elo = s_elo[m], ehi = s_ehi[m];
         const int extra = (int)(ehi - elo);
-        const bool check = final_ || !A.defer || A.amount + extra > (CAP - 32) / 2;
+        const bool check = !probing && (final_ || !A.defer || A.amount + extra > (CAP - 32) / 2);
         if (check) {
             bool ex = false;
             const int exo = s_exoff[m];
             if (exo >= 0) {                              // cached in LDS
                 for (int b0 = 0; b0 < extra; b0 += kWave) {          // wave-uniform
-                    const int e = b0 + lane < extra ? s_ex[wv][exo + b0 + lane] : -1;
+                    const int e = b0 + lane < extra ? s_exw[exo + b0 + lane] : -1;
                     const int ne = min(kWave, extra - b0);
                     for (int x = 0; x < ne; ++x) ex |= __builtin_amdgcn_readlane(e, x) == it;
                 }
@@ -1128,12 +1243,13 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
             rk += (vj > v || (vj == v && ij < it)) ? 1 : 0;
         }
         const bool val = v != -INFINITY;
-        const int rank = A.amount + (check ? 0 : extra);     // <= CAP - 32 (kMwMaxAmount)
+        const int rank = A.amount + (check || probing ? 0 : extra);   // <= CAP - 32 (kMwMaxAmount)
         bound = -INFINITY;
         if (__popcll(__builtin_amdgcn_ballot_w64(val)) >= rank) {
             const uint64_t at = __builtin_amdgcn_ballot_w64(val && rk == rank - 1);
             bound = readlane_f(v, (int)__builtin_ctzll(at)) - 2.f * s_m[m];
         }
+        bound = fmaxf(bound, readlane_f(lfloor, r));
         return __builtin_amdgcn_ballot_w64(val && v >= bound);
     };
     auto pos_in = [&](uint64_t mask) __attribute__((always_inline)) -> int {
@@ -1205,6 +1321,131 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
             if (bal[i]) insert_row(i, c0, acc, bic, bal[i]);       // wave-uniform
         settle();
     };
+    // Probe walk (A.n_probe > 0): the probe items (k_topk_probe) first, the
+    // users' excluded ones masked out.  The amount-th best s' of a user's list
+    // minus 2M is a floor under every later admission bound of the user: its
+    // `amount` probe items at or above tau have exact scores >= tau - M, so
+    // an item of the exact top `amount` has s >= tau - M, s' >= tau - 2M.  The
+    // lists are emptied afterwards (each probe item is scored again in its
+    // own split).  C3 model, a NumPy model of the admission rule: ~167
+    // admissions per user and split without it, ~3 with 512 probe items.
+    if (A.n_probe > 0) {
+        const int np = A.n_probe, G = A.probe_group;
+        // bit g of user r: probe item g is one of r's excluded items (an item
+        // e can only be probe item e / G)
+        for (int x = lane; x < 32 * kMwProbeWords; x += kWave) s_pexw[x] = 0ull;
+        asm volatile("" ::: "memory");
+        if (A.ex_ptr && q0 < A.nq) {
+            const int64_t elo = A.ex_ptr[q0], ehi = A.ex_ptr[min(q0 + 32, A.nq)];
+            constexpr int U = 4;                         // loads in flight per lane
+            for (int64_t b0 = elo; b0 < ehi; b0 += U * kWave) {        // wave-uniform
+                int32_t e[U], pg[U];
+#pragma unroll
+                for (int j = 0; j < U; ++j) {
+                    const int64_t t = b0 + j * kWave + lane;
+                    e[j] = t < ehi ? A.ex_items[t] : -1;
+                }
+#pragma unroll
+                for (int j = 0; j < U; ++j) {
+                    const int g = e[j] >= 0 && e[j] < A.n_items ? e[j] / G : np;
+                    pg[j] = g < np ? A.probe[g] : -2;
+                }
+#pragma unroll
+                for (int j = 0; j < U; ++j) {
+                    if (pg[j] == e[j]) {                 // rare: whose exclusion is it?
+                        const int64_t t = b0 + j * kWave + lane;
+                        int r = 0;
+                        while (r + 1 < 32 && q0 + r + 1 < A.nq && A.ex_ptr[q0 + r + 1] <= t) ++r;
+                        const int g = e[j] / G;
+                        atomicOr(reinterpret_cast<unsigned long long*>(
+                                     &s_pexw[r * kMwProbeWords + (g >> 6)]),
+                                 1ull << (g & 63));
+                    }
+                }
+            }
+        }
+        asm volatile("" ::: "memory");
+        probing = true;
+        auto load_p = [&](int t0) __attribute__((always_inline)) {
+            const int sl = t0 + c;
+            fetch(A.probe[sl < np ? sl : np - 1], 2);
+        };
+        load_p(0);
+        for (int t0 = 0; t0 < np; t0 += 32) {
+            f32x16 acc;
+            tile(acc);
+            const float bic = bi;
+            if (t0 + 32 < np) load_p(t0 + 32);
+            const int sl = t0 + c;
+            const bool have = sl < np;
+            const uint64_t* pw = s_pexw + (have ? sl >> 6 : 0);
+            uint64_t bal[16], any = 0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int r = (i & 3) + 8 * (i >> 2) + 4 * h;
+                const bool ex = (pw[r * kMwProbeWords] >> (sl & 63)) & 1ull;
+                const float sp = ((A.mu + bic) + ubu[i]) + acc[i];
+                bal[i] = __builtin_amdgcn_ballot_w64(have && !ex && sp >= uadm[i]);
+                any |= bal[i];
+            }
+            if (any) insert(t0, acc, bic, bal);
+        }
+        asm volatile("" ::: "memory");
+        for (int r = 0; r < 32; ++r) {
+            if (q0 + r >= A.nq) break;                   // wave-uniform
+            float v, bound;
+            int32_t it;
+            (void)compact(r, false, v, it, bound);
+            lfloor = writelane_f(bound, r, lfloor);
+        }
+        probing = false;
+        lcnt = 0;
+        ladm = q0 + c < A.nq ? lfloor : INFINITY;
+        if (A.defer != 2) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int r0 = (i & 3) + 8 * (i >> 2);
+                const float a0 = readlane_f(ladm, r0), a1 = readlane_f(ladm, r0 + 4);
+                uadm[i] = h ? a1 : a0;
+            }
+        }
+        asm volatile("" ::: "memory");
+    }
+    // The excluded ids of this wave's users in the split, packed into the
+    // wave's LDS area (users in order while they fit; the rest search HBM):
+    // a compaction then checks its list without a global-memory round trip.
+    {
+        int incl = ex_n;                                 // inclusive scan over lanes 0..31
+        for (int o = 1; o < 32; o <<= 1) {
+            const int t = __shfl_up(incl, o, kWave);
+            if (c >= o) incl += t;
+        }
+        const int off = incl - ex_n;
+        const bool fits = incl <= kMwExCap;
+        if (lane < 32) s_exoff[m0 + lane] = fits ? off : -1;
+        const uint64_t fm = __builtin_amdgcn_ballot_w64(lane < 32 && fits);
+        const int nfit = __popcll(fm);                   // users 0 .. nfit-1 are cached
+        const int ntot = nfit > 0 ? __builtin_amdgcn_readlane(incl, nfit - 1) : 0;
+        asm volatile("" ::: "memory");
+        // all loads in flight first, then the LDS stores
+        constexpr int kSteps = kMwExCap / kWave;
+        int32_t val[kSteps];
+#pragma unroll
+        for (int j = 0; j < kSteps; ++j) {
+            const int t = lane + kWave * j;
+            val[j] = 0;
+            if (t < ntot) {
+                int u = 0;                               // last user whose range starts at or before t
+                for (int r = 1; r < nfit; ++r) u += __builtin_amdgcn_readlane(off, r) <= t ? 1 : 0;
+                val[j] = A.ex_items[s_elo[m0 + u] + (t - s_exoff[m0 + u])];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kSteps; ++j)
+            if (lane + kWave * j < ntot) s_exw[lane + kWave * j] = val[j];
+    }
+    asm volatile("" ::: "memory");
+    load_b(ibeg);
     if constexpr (PIPE) {
         // Tile c+1's MFMAs interleaved with tile c's admission, row by row:
         // the 16 accumulator rows of tile c are compared and inserted
@@ -1217,21 +1458,12 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
         float ba, bb;
         tile(xa);
         ba = bi;
-        load_b(ibeg + 32, b, bi);
+        load_b(ibeg + 32);
+        // (the first part: the operands the MFMAs of rows 0..7 have read --
+        // f32: whole float4 groups among the first SEG / 2 columns; BF: the
+        // first NB / 2 column groups, whose 3 NB / 2 MFMAs come first)
         auto load_half = [&](int it0, int part) __attribute__((always_inline)) {
-            const int n = it0 + c;
-            const int nn = n < iend ? n : (ibeg < iend ? ibeg : 0);   // empty split: row 0
-            const float* qr = A.Q + (int64_t)nn * k;
-            if (part == 0) bi = A.Bi[nn];
-            // the first part: whole float4 groups among the columns the
-            // MFMAs of slices 0..7 have read (SEG / 2 of them)
-            constexpr int H4 = (SEG / 2) & ~3;
-#pragma unroll
-            for (int j = part == 0 ? 0 : H4; j < (part == 0 ? H4 : SEG); j += 4) {
-                const int c0 = h * SEG + j;
-                const float4 v = *reinterpret_cast<const float4*>(qr + (c0 < k ? c0 : 0));
-                b[j + 0] = v.x; b[j + 1] = v.y; b[j + 2] = v.z; b[j + 3] = v.w;
-            }
+            fetch(item_of(it0), part);
         };
         auto step = [&](int c0, f32x16& x, float& bx, f32x16& y, float& by)
                         __attribute__((always_inline)) {
@@ -1242,8 +1474,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
 #pragma unroll
-                for (int s = i * SEG / 16; s < (i + 1) * SEG / 16; ++s)
-                    y = __builtin_amdgcn_mfma_f32_32x32x2f32(a[s], b[s], y, 0, 0, 0);
+                for (int m = i * NM / 16; m < (i + 1) * NM / 16; ++m) mfma_m(y, m);
                 if (i == 7) load_half(c0 + 64, 0);       // tile c+2, columns of the first half
                 const float sp = ((A.mu + bx) + ubu[i]) + x[i];
                 const uint64_t bal = __builtin_amdgcn_ballot_w64(have && sp >= uadm[i]);
@@ -1261,7 +1492,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
             f32x16 acc;
             tile(acc);
             const float bic = bi;
-            if (c0 + 32 < iend) load_b(c0 + 32, b, bi);
+            if (c0 + 32 < iend) load_b(c0 + 32);
             uint64_t bal[16];
             if (admit(c0, acc, bic, bal)) insert(c0, acc, bic, bal);
         }
@@ -1469,6 +1700,8 @@ struct TopkLaunch {
     }
 };
 
+void touch_topk(hipStream_t s) { hipLaunchKernelGGL(k_touch<6>, dim3(1), dim3(64), 0, s); }
+
 }  // namespace mf
 
 #include "mf_dispatch.hpp"
@@ -1512,6 +1745,8 @@ extern "C" int mf_topk(const int32_t* query_users, int32_t n_query, double globa
 
 // ---------------------------------------------------------------- MFMA filter ABI
 static int mm_seg(int k) { return ((k / 2 + 3) / 4) * 4; }
+// bytes per item of k_topk_split_q's rows at the largest k (2 halves x hi / lo x NB groups)
+constexpr size_t kMwSplitRowBytes = 2 * 2 * ((kMmMaxK / 2 + 7) / 8) * sizeof(bf16x8);
 
 extern "C" int32_t mf_topk_mm_supported(int32_t n_factors, int32_t kernel, int32_t dtype,
                                         int32_t amount) {
@@ -1525,7 +1760,24 @@ extern "C" size_t mf_topk_mm_workspace_bytes(int32_t n_query, int32_t n_items) {
     const size_t ns = (size_t)std::max(topk_mm_splits(n_query, n_items),
                                        topk_mw_splits(n_query, n_items));
     return 16 + 4 * (size_t)n_query + 4 * (size_t)n_query * ns +
-           8 * (size_t)n_query * ns * kMmCap;
+           8 * (size_t)n_query * ns * kMmCap + 4 * (size_t)kMwProbe + 16 +
+           kMwSplitRowBytes * (size_t)n_items;
+}
+
+// k_topk_mw's operands: bf16 hi + lo parts on the bf16 MFMA (BF, 5.3x fewer
+// matrix cycles than the f32 MFMA per tile) -- MF_TOPK_BF16=0: f32 (probes)
+inline bool topk_mw_bf16() {
+    const char* e = std::getenv("MF_TOPK_BF16");
+    return !(e && std::atoi(e) == 0);
+}
+
+// k_topk_mw's probe items: one per group of >= 128 item ids, at most kMwProbe
+// (C3, 100K items: 511 groups of 196; the caller trims the count so that no
+// group is empty).  MF_TOPK_PROBE=0: none (probes, A/B).
+inline int topk_mw_probes(int32_t n_items) {
+    if (const char* e = std::getenv("MF_TOPK_PROBE"))
+        if (std::atoi(e) == 0) return 0;
+    return std::min<int32_t>(kMwProbe, n_items / 128);
 }
 
 extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double global_mean,
@@ -1568,6 +1820,19 @@ extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double gl
     a.part_s = (float*)(a.part_n + (size_t)n_query * a.n_splits);
     a.part_id = (int32_t*)(a.part_s + (size_t)n_query * a.n_splits * kMmCap);
     a.overflow = overflow;
+    a.probe = (int32_t*)(a.part_id + (size_t)n_query * a.n_splits * kMmCap);
+    {
+        const uintptr_t qs = reinterpret_cast<uintptr_t>(a.probe + kMwProbe);
+        a.Qs = reinterpret_cast<const bf16x8*>((qs + 15) & ~(uintptr_t)15);
+    }
+    const char* pe = std::getenv("MF_TOPK_MM_PIPE");
+    const bool pipe = pe ? std::atoi(pe) != 0 : true;
+    const bool bf = mw && pipe && topk_mw_bf16();
+    a.n_probe = mw ? topk_mw_probes(n_items) : 0;
+    a.probe_group = a.n_probe > 0 ? (n_items + a.n_probe - 1) / a.n_probe : 0;
+    // every group non-empty (C3: 512 groups of 196 ids would leave the last
+    // one past n_items; 511 are used)
+    if (a.n_probe > 0) a.n_probe = (n_items + a.probe_group - 1) / a.probe_group;
     {
         const char* e = std::getenv("MF_TOPK_MM_DEFER");             // probes
         a.defer = e ? std::atoi(e) : 0;
@@ -1577,17 +1842,30 @@ extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double gl
         const int fv = f ? std::atoi(f) : kMwCap - 32;
         a.fill = std::max(amount + 1, std::min(fv, kMwCap - 32));
     }
-    MF_HIP_CHECK(hipMemsetAsync(stats, 0, 8, st));
-    hipLaunchKernelGGL(k_topk_mm_stats, dim3((unsigned)((n_items + kBlock - 1) / kBlock)),
-                       dim3(kBlock), 0, st, a.Q, a.Bi, n_items, n_factors, stats);
+    MF_HIP_CHECK(hipMemsetAsync(stats, 0, 16, st));
+    const unsigned nb_stats = (unsigned)((n_items + kBlock - 1) / kBlock +
+                                         (a.n_probe > 0 ? (n_query + kBlock - 1) / kBlock : 0));
+    hipLaunchKernelGGL(k_topk_mm_stats, dim3(nb_stats), dim3(kBlock), 0, st, a.Q, a.Bi, n_items,
+                       n_factors, stats, query_users, n_query, a.P);
+    if (a.n_probe > 0)
+        hipLaunchKernelGGL(k_topk_probe,
+                           dim3((unsigned)((a.n_probe + kWavesPerBlock - 1) / kWavesPerBlock)),
+                           dim3(kBlock), 0, st, a.Q, a.Bi, n_items, n_factors, a.probe_group,
+                           a.n_probe, (const float*)stats, const_cast<int32_t*>(a.probe));
+    if (bf) {
+        const int seg = mm_seg(n_factors), nb = (seg + 7) / 8;
+        const int64_t nt = (int64_t)n_items * 2 * nb;
+        hipLaunchKernelGGL(k_topk_split_q, dim3((unsigned)((nt + kBlock - 1) / kBlock)),
+                           dim3(kBlock), 0, st, a.Q, n_items, n_factors, seg, nb,
+                           const_cast<bf16x8*>(a.Qs));
+    }
     const int nt = topk_mm_nt();
     const dim3 grid((unsigned)a.n_splits, (unsigned)((n_query + 32 * nt - 1) / (32 * nt)));
-    const char* pe = std::getenv("MF_TOPK_MM_PIPE");
-    const bool pipe = pe ? std::atoi(pe) != 0 : true;
     const dim3 grid_mw((unsigned)a.n_splits, (unsigned)((n_query + kMwUsers - 1) / kMwUsers));
 #define MF_MM_LAUNCH(S)                                                                        \
     if (mw) {                                                                                 \
-        if (pipe) hipLaunchKernelGGL((k_topk_mw<S, true>), grid_mw, dim3(kBlock), 0, st, a);   \
+        if (pipe && bf) hipLaunchKernelGGL((k_topk_mw<S, true, true>), grid_mw, dim3(kBlock), 0, st, a); \
+        else if (pipe) hipLaunchKernelGGL((k_topk_mw<S, true>), grid_mw, dim3(kBlock), 0, st, a); \
         else hipLaunchKernelGGL((k_topk_mw<S, false>), grid_mw, dim3(kBlock), 0, st, a);      \
     } else if (nt == 1) {                                                                            \
         if (pipe) hipLaunchKernelGGL((k_topk_mm<S, true, 1>), grid, dim3(kBlock), 0, st, a);  \

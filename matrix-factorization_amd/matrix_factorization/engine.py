@@ -819,7 +819,22 @@ class SGDEngine:
         # now, not in the first epoch
         if self.n:
             self._ensure_strata_ws(plan.B, plan.n_strata)
+            self._prime_strata(plan)
         return plan
+
+    def _prime_strata(self, pl) -> None:
+        """The launcher's one-time runtime work for this plan's kernels
+        (MF_FLAG_PREPARE: kernel attributes, the co-residency query -- no
+        launch, the parameters untouched), so that it is not paid inside
+        fit()'s first epochs."""
+        subs = pl.phases if isinstance(pl, PhasedStrata) else [pl]
+        for sub in subs:
+            if sub.n_positions == 0:
+                continue
+            seq = np.arange(sub.n_strata, dtype=np.int32)
+            flags = self._strata_flags(sub, None) | _lib.MF_FLAG_PREPARE
+            self._run_strata(sub, seq, 0, 0.0, 0.0, True, True, flags, None, None, self.Q,
+                             self.bi, self.n_items)
 
     # relabelled plans, "regroupings" (DESIGN.md section 3.1): K - 1 more
     # plans of the same B and classes over randomly relabelled users and

@@ -14,6 +14,12 @@ Three keyword arguments are new and default to the reference's behaviour:
               "strata": the stratified sweep (users x items cut into B x B
               blocks, item slabs resident in LDS; mf_strata.hpp), also a
               valid sequential order per epoch -- the throughput setting.
+              Known deviation: a different order trains to a slightly
+              different model.  At C3 (20 epochs) the default strata plan
+              ends +0.36e-5 train RMSE over the mean of the reference's
+              random orders (24 draws, round 5; +0.64e-5 pooled with round
+              4's 48, about 2.7 standard errors), where the reference's own
+              run-to-run spread is ~1e-5; "exact" has no such gap.
 ``device``    HIP device ("cuda", "cuda:1", ...); None = current device.
 ``distributed`` False (default) or True: process-group mode.  When
               torch.distributed is initialised with world_size > 1, every
@@ -30,7 +36,13 @@ Three keyword arguments are new and default to the reference's behaviour:
 ``strata_regroup``  schedule "strata" only: relabelled plans drawn epoch by
               epoch (which users share a range, which items a slab),
               "auto" (default: 2 for the linear kernel's multi-class plans,
-              else 1) or 1..4.
+              else 1) or 1..4.  Each relabelled plan
+              costs device memory: its relabelled user / item ids (8 B per
+              rating), its padded copy of the ratings in plan order (4 + 4 +
+              itemsize bytes per position) and a second set of P, Q, b_u,
+              b_i -- at C3 ~2.4 GB (float32) / 3.1 GB (float64) per plan.
+              strata_regroup=1 avoids it (the plan's order then sits
+              further from the reference's, section 3.1).
 ``exchange``  process-group mode only: "rotate" (default; exact -- items are
               cut into one range per rank and the ranges are passed round the
               ring between sub-epochs, so every rating is applied with the

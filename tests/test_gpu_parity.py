@@ -353,11 +353,14 @@ def _topk_both(eng, users, amount, ex_ptr=None, ex_items=None):
     return mi, ms, q["items"].cpu().numpy(), q["scores"].cpu().numpy(), fell_back
 
 
+@pytest.mark.parametrize("bf16", ["1", "0"])
 @pytest.mark.parametrize("k,amount", [(8, 10), (20, 1), (32, 64), (64, 10), (64, 64)])
-def test_topk_mfma_filter_equals_exact(k, amount):
+def test_topk_mfma_filter_equals_exact(k, amount, bf16, monkeypatch):
     """mf_topk_mm (MFMA scores only select candidates; survivors rescored
     with predict's arithmetic) returns exactly mf_topk's ids and scores:
-    ragged item / user counts, unknown users (-1), CSR exclusions."""
+    ragged item / user counts, unknown users (-1), CSR exclusions -- with
+    k_topk_mw's operands as bf16 hi + lo parts (the default) and as f32."""
+    monkeypatch.setenv("MF_TOPK_BF16", bf16)
     nu, ni = 900, 5003
     eng = _topk_engine(k, nu, ni, 40 + k)
     rs = np.random.RandomState(k)
@@ -385,6 +388,45 @@ def test_topk_mfma_filter_ties_and_overflow():
     assert np.array_equal(ms, es)
     ids, sc = eng.topk(users, 64)
     assert np.array_equal(ids, ei)
+
+
+@pytest.mark.parametrize("bf16", ["1", "0"])
+@pytest.mark.parametrize("ni", [20000, 65600])
+def test_topk_probe_floor_with_excluded_top_items(ni, bf16, monkeypatch):
+    """k_topk_mw's probe walk (the best item of each group of ids scored
+    first; the amount-th best s' of a user's non-excluded probe items, less
+    2M, floors every admission bound) under exclusions aimed at it: users
+    whose exact top-40 items are all excluded (so are most probe items that
+    rank high for them), a user left with 5 candidates (fewer than amount:
+    no floor, -1 padding) and one with every item excluded.  Same ids and
+    scores as mf_topk, no excluded item returned.  65600 items: 512 groups of
+    129 ids would leave the last group empty (the probe count is trimmed to
+    509; an empty group once read a row past the end of Q)."""
+    monkeypatch.setenv("MF_TOPK_BF16", bf16)
+    k, nu, amount = 64, 400, 10
+    eng = _topk_engine(k, nu, ni, 23)
+    rs = np.random.RandomState(5)
+    users = rs.choice(nu, 260, replace=False).astype(np.int32)
+    top, _ = eng.topk(users, 40)
+    lists = []
+    for q in range(len(users)):
+        if q == 7:
+            ex = np.setdiff1d(np.arange(ni), rs.choice(ni, 5, replace=False))
+        elif q == 8:
+            ex = np.arange(ni)
+        elif q % 2:
+            ex = np.union1d(top[q], rs.choice(ni, 30, replace=False))
+        else:
+            ex = rs.choice(ni, rs.randint(0, 50), replace=False)
+        lists.append(np.sort(ex).astype(np.int32))
+    ex_ptr = np.concatenate([[0], np.cumsum([len(x) for x in lists])]).astype(np.int64)
+    ex_items = np.concatenate(lists).astype(np.int32)
+    mi, ms, ei, es, _ = _topk_both(eng, users, amount, ex_ptr, ex_items)
+    assert np.array_equal(mi, ei)
+    assert np.array_equal(np.nan_to_num(ms, nan=-7.0), np.nan_to_num(es, nan=-7.0))
+    assert (mi[7] >= 0).sum() == 5 and (mi[8] < 0).all()
+    for q in range(len(users)):
+        assert not set(mi[q][mi[q] >= 0]) & set(lists[q])
 
 
 @pytest.mark.parametrize("mfma", [True, False])

@@ -576,15 +576,14 @@ def test_bench_traffic_lookup_is_keyed_on_world_and_emulation():
     sys.path.insert(0, ROOT)
     import bench
 
-    got = bench.traffic_from_profiles("c3", 1, "strata_persistent", "float32",
-                                      "k_sgd_strata_epoch")
+    kern = "k_sgd_strata_stream"                              # the default C3 kernel
+    got = bench.traffic_from_profiles("c3", 1, "strata_persistent", "float32", kern)
     assert got is not None and got > 1e9                      # the committed N = 1 counters
+    assert bench.traffic_from_profiles("c3", 1, "strata_persistent", "float32", kern,
+                                       emulate=8) is None
+    assert bench.traffic_from_profiles("c3", 8, "strata_persistent", "float32", kern) is None
     assert bench.traffic_from_profiles("c3", 1, "strata_persistent", "float32",
-                                       "k_sgd_strata_epoch", emulate=8) is None
-    assert bench.traffic_from_profiles("c3", 8, "strata_persistent", "float32",
-                                       "k_sgd_strata_epoch") is None
-    assert bench.traffic_from_profiles("c3", 1, "strata_persistent", "float32",
-                                       "k_sgd_strata") is None     # another kernel
+                                       "k_sgd_strata_epoch") is None     # another kernel
 
 
 @pytest.mark.parametrize("chunks", [1, 2, 5, 16])

@@ -22,6 +22,8 @@ Designs (--designs, any of):
   rotrel<K>           the rotation over K item relabellings, one drawn per
                       epoch (which items share a range changes epoch to
                       epoch; the ranges are all-gathered anyway);
+  rotc<C>[b<B>]       the rotation with sub-block plans of C user-range classes
+                      (and B blocks): the stream kernel applies from C = 2;
   delta<M>s<S>        user-sharded replicas, the stratum order of each rank's
                       epoch cut into M rounds; after every round the item
                       deltas of all ranks are summed (all_reduce) and added
@@ -143,7 +145,7 @@ def main():
         return out
 
     # ------------------------------------------------------------- designs
-    def run_rotate(name, sub=1, relabel=1):
+    def run_rotate(name, sub=1, relabel=1, classes=None, blocks=None):
         parts = shard_engines(sub)
         perms = [np.arange(ni)] + [np.random.RandomState(5150 + q).permutation(ni)
                                    for q in range(relabel - 1)]
@@ -153,7 +155,9 @@ def main():
             for key, (a, b, us, is_, rs_) in parts.items():
                 e = SGDEngine(us, pi[is_].astype(np.int32), rs_, b - a, ni, k, kernel, "float32",
                               dev, **hyp)
-                e.prepare_strata(item_bounds=item_ranges(pi[i].astype(np.int32), ni, W))
+                e.prepare_strata(n_blocks=blocks,
+                                 item_bounds=item_ranges(pi[i].astype(np.int32), ni, W),
+                                 classes=classes)
                 engs[key] = e
             sets.append(engs)
         dpi = [torch.from_numpy(p).to(dev) for p in perms]
@@ -289,6 +293,9 @@ def main():
             run_rotate(d, sub=int(d[6:]))
         elif d.startswith("rotrel"):
             run_rotate(d, relabel=int(d[6:]))
+        elif d.startswith("rotc"):                 # rotc<C>[b<B>]: sub-block plans of C classes
+            cc, _, bb = d[4:].partition("b")
+            run_rotate(d, classes=int(cc), blocks=int(bb) if bb else None)
         elif d.startswith("delta"):
             m, sc = d[5:].split("s")
             run_delta(d, int(m), default_delta_scale(W) if sc == "d" else float(sc))
