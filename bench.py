@@ -335,10 +335,26 @@ def run_topk(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
     ts = 4 if args.dtype == "float32" else 8
     achieved = scores * k * ts / elapsed / 1e9
     mmk = "k_topk_mw" if amount <= 16 and os.environ.get("MF_TOPK_MW") != "0" else "k_topk_mm"
-    path = (f"MFMA filter ({mmk} + k_topk_mm_merge, exact rescoring)" if mm else
+    path = (f"MFMA filter ({mmk}{' bf16 hi/lo' if mmk == 'k_topk_mw' and os.environ.get('MF_TOPK_BF16') != '0' else ''}"
+            f" + k_topk_mm_merge, exact rescoring)" if mm else
             "two-stage (keys in HBM)" if os.environ.get("MF_TOPK_TWO_STAGE") == "1"
             else "fused (k_topk_fused + k_topk_merge)")
-    if mm:
+    bf16 = mmk == "k_topk_mw" and os.environ.get("MF_TOPK_BF16") != "0" and \
+        os.environ.get("MF_TOPK_MM_PIPE") != "0"
+    if mm and bf16:
+        # k_topk_mw<.., BF>: three bf16 32x32x16 MFMAs (lo x hi, hi x lo,
+        # hi x hi) per 16 columns, so 3 x 2k executed flops per score against
+        # the dense bf16 peak; f32_equivalent = the 2k algorithmic flops
+        # against the f32 MFMA peak (the round-4 form's roofline)
+        tf = scores * 2 * k / elapsed / 1e12
+        roof = {"bound": "mfma", "achieved": 3 * tf, "peak": 2500.0, "unit": "TFLOP/s",
+                "frac": 3 * tf / 2500.0, "traffic": None, "kernel": mmk,
+                "f32_equivalent": {"achieved": tf, "peak": 157.3, "frac": tf / 157.3},
+                "note": "6k executed flops per score on v_mfma_f32_32x32x16_bf16 (hi/lo split "
+                        "operands; dense bf16 peak); device time of the mf_topk_mm launches "
+                        "(inputs resident) incl. the stats / probe / split pre-passes and the "
+                        "merge"}
+    elif mm:
         tf = scores * 2 * k / elapsed / 1e12
         roof = {"bound": "mfma", "achieved": tf, "peak": 157.3, "unit": "TFLOP/s",
                 "frac": tf / 157.3, "traffic": None, "kernel": mmk,

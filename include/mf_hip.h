@@ -107,10 +107,12 @@ enum {
 
 const char* mf_last_error(void);
 int mf_abi_version(void);
-/* One empty kernel launch on `stream`: makes the runtime load this library's
- * code object for the current device now (the engine calls it while it is
- * built) instead of inside the first training epoch. */
-int mf_warmup(void* stream);
+/* One empty kernel launch per translation unit of this library on `stream`,
+ * and one cooperative launch: makes the runtime load the code objects for
+ * the current device now (the engine calls it while it is built) instead of
+ * inside the first training epoch.  flags & MF_FLAG_NO_COOP: no cooperative
+ * launch (rocprofv3's dispatch interception crashes on one). */
+int mf_warmup(int32_t flags, void* stream);
 /* Up to MF_PERMUTE_MAX_JOBS row arrays permuted in one launch (the relabelled
  * strata plans' parameter moves): job j has n_rows[j]
  * rows of row_bytes[j] bytes (a multiple of 4); mode 0 gathers dst[r] =

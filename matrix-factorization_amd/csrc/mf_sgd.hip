@@ -288,7 +288,7 @@ extern "C" size_t mf_strata_workspace_bytes(int32_t n_blocks, int32_t n_seq) {
 // library), which otherwise lands in the first training epoch.
 __global__ void k_warmup() {}
 
-extern "C" int mf_warmup(void* stream) {
+extern "C" int mf_warmup(int32_t flags, void* stream) {
     const hipStream_t s = (hipStream_t)stream;
     const LaunchTrace lt;
     hipLaunchKernelGGL(k_warmup, dim3(1), dim3(64), 0, s);
@@ -303,7 +303,7 @@ extern "C" int mf_warmup(void* stream) {
     touch_topk(s);
     touch_als(s);
     lt.mark("warmup: other units");
-    {   // the cooperative launch path (persistent sweeps)
+    if (!(flags & MF_FLAG_NO_COOP)) {   // the cooperative launch path (persistent sweeps)
         void* no_args[1] = {nullptr};
         (void)hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_warmup), dim3(1),
                                          dim3(64), no_args, 0u, s);

@@ -614,29 +614,46 @@ __global__ __launch_bounds__(kBlock) void k_topk_probe(const float* __restrict__
     if (lane == 0) probe[g] = bid == 0x7fffffff ? (int32_t)lo : bid;   // (NaN keys: the first)
 }
 
-// k_topk_split_q: the item rows as k_topk_mw<.., BF> reads them -- item x,
-// lane half h: NB groups of 8 hi parts, then their NB lo parts (x = hi + lo
-// + e, hi = bf16(x), lo = bf16(x - hi)); group s, element j = column
-// h seg + 8 s + j (zero past seg or k).  One thread per (item, half, group).
+// k_topk_split_q: the item rows as k_topk_mw<.., BF> loads them, in tiles of
+// 32 items in the MFMA operand layout.  Element j of lane (c, h)'s fragment
+// for column group g is column h seg + 8 g + j (zero past seg or k) of the
+// tile's item c, split x = hi + lo + e (hi = bf16(x), lo = bf16(x - hi));
+// tile T, group g, part t (0 hi, 1 lo) holds 64 lane-ordered 16-B chunks
+// (lane = 32 h + c), so one load instruction of a wave reads 1 KB of whole
+// cache lines.  Tiles 0 .. n_tiles-1 are items 32 T + c (zero past n_items),
+// the n_ptiles after them the probe items probe[32 T' + c] (zero past
+// n_probe).  One thread per (tile, group, lane).
 __global__ __launch_bounds__(kBlock) void k_topk_split_q(const float* __restrict__ Q,
                                                          int32_t n_items, int32_t k, int32_t seg,
-                                                         int32_t nb, bf16x8* __restrict__ Qs) {
+                                                         int32_t nb, int32_t n_tiles,
+                                                         const int32_t* __restrict__ probe,
+                                                         int32_t n_probe, int32_t n_ptiles,
+                                                         bf16x8* __restrict__ Qs) {
     const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (t >= (int64_t)n_items * 2 * nb) return;
-    const int64_t it = t / (2 * nb);
-    const int rem = (int)(t - it * 2 * nb), h = rem / nb, g = rem % nb;
+    if (t >= (int64_t)(n_tiles + n_ptiles) * nb * 64) return;
+    const int64_t T = t / (nb * 64);
+    const int rem = (int)(t - T * nb * 64), g = rem / 64, lane = rem % 64;
+    const int c = lane & 31, h = lane >> 5;
+    int64_t it;
+    if (T < n_tiles) {
+        it = T * 32 + c;
+        if (it >= n_items) it = -1;
+    } else {
+        const int64_t sl = (T - n_tiles) * 32 + c;
+        it = sl < n_probe ? probe[sl] : -1;
+    }
     bf16x8 hi, lo;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
         const int ci = 8 * g + j, col = h * seg + ci;
-        const float x = ci < seg && col < k ? Q[it * k + col] : 0.f;
+        const float x = it >= 0 && ci < seg && col < k ? Q[it * k + col] : 0.f;
         const __bf16 xh = (__bf16)x;
         hi[j] = xh;
         lo[j] = (__bf16)(x - (float)xh);
     }
-    bf16x8* o = Qs + (it * 2 + h) * 2 * nb;
-    o[g] = hi;
-    o[nb + g] = lo;
+    bf16x8* o = Qs + ((T * nb + g) * 2) * 64 + lane;
+    o[0] = hi;
+    o[64] = lo;
 }
 
 // (score desc, id asc) bitonic sort of n (power of two) float-keyed entries
@@ -1058,7 +1075,8 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
     const int m0 = 32 * wv;                              // this wave's users: m0 .. m0 + 31
     const int q0 = blockIdx.y * kMwUsers + m0;
     const int k = A.k;
-    const int64_t span = ((int64_t)A.n_items + A.n_splits - 1) / A.n_splits;
+    // splits start on 32-item tiles (the BF operand tiles, k_topk_split_q)
+    const int64_t span = (((int64_t)A.n_items + A.n_splits - 1) / A.n_splits + 31) & ~(int64_t)31;
     const int ibeg = (int)min((int64_t)A.n_items, span * split);
     const int iend = (int)min((int64_t)A.n_items, span * (split + 1));
     const float qmax = A.stats[0], bimax = A.stats[1];
@@ -1143,16 +1161,21 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
     // B operands (and b_i) of item nn: part 0 / 1 = those the first / second
     // half of a tile's MFMAs read (the MFMAs of rows 0..7 / 8..15 in the
     // pipelined loop), 2 = all
+    const int n_tiles = (A.n_items + 31) >> 5;
+    // BF: tile tb's operands (k_topk_split_q's layout: lane-ordered chunks)
+    auto fetch_bf = [&](const bf16x8* tb, int part) __attribute__((always_inline)) {
+        constexpr int HB = NB / 2;
+#pragma unroll
+        for (int s2 = part == 1 ? HB : 0; s2 < (part == 0 ? HB : NB); ++s2) {
+            bh[s2] = tb[(2 * s2) * 64 + lane];
+            bl[s2] = tb[(2 * s2 + 1) * 64 + lane];
+        }
+    };
     auto fetch = [&](int nn, int part) __attribute__((always_inline)) {
         if (part != 1) bi = A.Bi[nn];
         if constexpr (BF) {
-            const bf16x8* qs = A.Qs + ((int64_t)nn * 2 + h) * 2 * NB;
-            constexpr int HB = NB / 2;
-#pragma unroll
-            for (int s2 = part == 1 ? HB : 0; s2 < (part == 0 ? HB : NB); ++s2) {
-                bh[s2] = qs[s2];
-                bl[s2] = qs[NB + s2];
-            }
+            // tile of the walk position (it0 = 32 T, nn its lane's item or the
+            // clamped one): the caller passes the tile through fetch_tile
         } else {
             const float* qr = A.Q + (int64_t)nn * k;
             constexpr int H4 = (SEG / 2) & ~3;
@@ -1168,7 +1191,21 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
         const int n = it0 + c;
         return n < iend ? n : (ibeg < iend ? ibeg : 0);  // empty split: row 0
     };
-    auto load_b = [&](int it0) __attribute__((always_inline)) { fetch(item_of(it0), 2); };
+    // the walk's tile at it0 (a multiple of 32: splits start on tiles);
+    // past the split's end: its first tile (never admitted, `have`)
+    auto tile_ptr = [&](int it0) __attribute__((always_inline)) -> const bf16x8* {
+        int T = (it0 < iend ? it0 : ibeg) >> 5;
+        T = T < n_tiles ? T : n_tiles - 1;
+        return A.Qs + (int64_t)T * NB * 2 * 64;
+    };
+    auto fetch_tile = [&](int it0, int part) __attribute__((always_inline)) {
+        if (part != 1) bi = A.Bi[item_of(it0)];
+        fetch_bf(tile_ptr(it0), part);
+    };
+    auto load_b = [&](int it0) __attribute__((always_inline)) {
+        if constexpr (BF) fetch_tile(it0, 2);
+        else fetch(item_of(it0), 2);
+    };
     // the NM MFMAs of a tile; mfma_m issues the m-th (BF: for each 16 columns
     // lo x hi, hi x lo, hi x hi)
     constexpr int NM = BF ? 3 * NB : SEG;
@@ -1368,7 +1405,12 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
         probing = true;
         auto load_p = [&](int t0) __attribute__((always_inline)) {
             const int sl = t0 + c;
-            fetch(A.probe[sl < np ? sl : np - 1], 2);
+            if constexpr (BF) {       // the probe tiles follow the item tiles
+                bi = A.Bi[A.probe[sl < np ? sl : np - 1]];
+                fetch_bf(A.Qs + (int64_t)(n_tiles + (t0 >> 5)) * NB * 2 * 64, 2);
+            } else {
+                fetch(A.probe[sl < np ? sl : np - 1], 2);
+            }
         };
         load_p(0);
         for (int t0 = 0; t0 < np; t0 += 32) {
@@ -1463,7 +1505,8 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
         // f32: whole float4 groups among the first SEG / 2 columns; BF: the
         // first NB / 2 column groups, whose 3 NB / 2 MFMAs come first)
         auto load_half = [&](int it0, int part) __attribute__((always_inline)) {
-            fetch(item_of(it0), part);
+            if constexpr (BF) fetch_tile(it0, part);
+            else fetch(item_of(it0), part);
         };
         auto step = [&](int c0, f32x16& x, float& bx, f32x16& y, float& by)
                         __attribute__((always_inline)) {
@@ -1761,7 +1804,7 @@ extern "C" size_t mf_topk_mm_workspace_bytes(int32_t n_query, int32_t n_items) {
                                        topk_mw_splits(n_query, n_items));
     return 16 + 4 * (size_t)n_query + 4 * (size_t)n_query * ns +
            8 * (size_t)n_query * ns * kMmCap + 4 * (size_t)kMwProbe + 16 +
-           kMwSplitRowBytes * (size_t)n_items;
+           kMwSplitRowBytes * (32 * (((size_t)n_items + 31) / 32) + kMwProbe);
 }
 
 // k_topk_mw's operands: bf16 hi + lo parts on the bf16 MFMA (BF, 5.3x fewer
@@ -1854,10 +1897,11 @@ extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double gl
                            a.n_probe, (const float*)stats, const_cast<int32_t*>(a.probe));
     if (bf) {
         const int seg = mm_seg(n_factors), nb = (seg + 7) / 8;
-        const int64_t nt = (int64_t)n_items * 2 * nb;
+        const int n_tiles = (n_items + 31) / 32, n_ptiles = (a.n_probe + 31) / 32;
+        const int64_t nt = (int64_t)(n_tiles + n_ptiles) * nb * 64;
         hipLaunchKernelGGL(k_topk_split_q, dim3((unsigned)((nt + kBlock - 1) / kBlock)),
-                           dim3(kBlock), 0, st, a.Q, n_items, n_factors, seg, nb,
-                           const_cast<bf16x8*>(a.Qs));
+                           dim3(kBlock), 0, st, a.Q, n_items, n_factors, seg, nb, n_tiles,
+                           a.probe, a.n_probe, n_ptiles, const_cast<bf16x8*>(a.Qs));
     }
     const int nt = topk_mm_nt();
     const dim3 grid((unsigned)a.n_splits, (unsigned)((n_query + 32 * nt - 1) / (32 * nt)));

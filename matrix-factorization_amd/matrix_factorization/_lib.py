@@ -108,7 +108,7 @@ SIGNATURES = {
         _P, _P, _P, _I32, _F64, _P, _P, _P, _P, _I32, _I32, _F64, _P, _P]),
     "mf_replica_delta": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _P]),
     "mf_replica_apply": (ctypes.c_int, [_P, _P, _I64, _I32, _F64, _P]),
-    "mf_warmup": (ctypes.c_int, [_P]),
+    "mf_warmup": (ctypes.c_int, [ctypes.c_int32, _P]),
     "mf_permute_rows": (ctypes.c_int, [_I32, _P, _P, _P, _P, _P, _I32, _P]),
     "mf_sched_levels": (ctypes.c_int, [
         _P, _P, _I64, _P, _I32, _I32, _I32, _I32, _P, _P, _I64, _P]),

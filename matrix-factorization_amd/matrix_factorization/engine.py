@@ -78,7 +78,9 @@ def _warm_device(dev: torch.device) -> None:
     if dev.type != "cuda" or dev.index in _WARMED:
         return
     with torch.cuda.device(dev):
-        _lib.call("mf_warmup", _VOID(torch.cuda.current_stream(dev).cuda_stream))
+        # (no cooperative launch under rocprofv3: its interception crashes)
+        _lib.call("mf_warmup", _lib.MF_FLAG_NO_COOP if _under_rocprofiler() else 0,
+                  _VOID(torch.cuda.current_stream(dev).cuda_stream))
     _WARMED.add(dev.index)
 
 

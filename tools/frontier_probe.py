@@ -22,6 +22,7 @@ Designs (--designs, any of):
   rotrel<K>           the rotation over K item relabellings, one drawn per
                       epoch (which items share a range changes epoch to
                       epoch; the ranges are all-gathered anyway);
+  rotcls<M>rel<K>     both of the above;
   rotc<C>[b<B>]       the rotation with sub-block plans of C user-range classes
                       (and B blocks): the stream kernel applies from C = 2;
   delta<M>s<S>        user-sharded replicas, the stratum order of each rank's
@@ -289,6 +290,9 @@ def main():
     for d in args.designs:
         if d == "rotate":
             run_rotate(d)
+        elif d.startswith("rotcls") and "rel" in d:       # rotcls<M>rel<K>: both
+            m, kk = d[6:].split("rel")
+            run_rotate(d, sub=int(m), relabel=int(kk))
         elif d.startswith("rotcls"):
             run_rotate(d, sub=int(d[6:]))
         elif d.startswith("rotrel"):
