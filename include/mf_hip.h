@@ -96,11 +96,6 @@ enum {
                                  (kernel attributes, the co-residency query),
                                  so the first epoch does not pay it; the
                                  parameter pointers are not touched */
-    MF_FLAG_PAIRS = 4096,     /* 8-wave plans of FP32 rows one 16-B vector per
-                                 lane in lane groups of 8 (k <= 32): run by 4
-                                 waves whose lane groups apply two slots each
-                                 (the same plan and order, two independent
-                                 ratings per lane group and step) */
     /* mf_sgd_epoch_strata: bits 24..27 = C - 1, the plan's user-range classes
        (mf_strata_plan_build_classes; 0 = C = 1, the plain B x B plan) */
     MF_FLAG_CLASSES_SHIFT = 24

@@ -1443,12 +1443,6 @@ struct StrataRun {
                         return go<W, GS2, V2, KERN, strata_group_slots<T, W, GS2, V2>(), 4>();
                     }
                 }
-                // MF_FLAG_PAIRS: the same 64 slots on 4 waves, two per lane group
-                if constexpr (S == 1 && GS == 8 && std::is_same<T, float>::value) {
-                    static_assert(strata_slots<T, W, GS, V, 8>() == 4 * 2 * (kWave / GS),
-                                  "pairs form: same slot count");
-                    if (p.flags & MF_FLAG_PAIRS) return go<W, GS, V, KERN, 2, 4>();
-                }
                 return go<W, GS, V, KERN, S, 8>();
             }
         }
@@ -1522,8 +1516,7 @@ struct StrataRun {
             p.ws_bytes >= strata_ws_bytes(p.B, p.n_seq) && a.p_bytes < (uint64_t)kBufDrop &&
             strata_class_cycle(p.seq, p.n_seq, a.cls)) {
             // (the deep pipeline exists for the 16- and 8-wave kernels)
-            // (the pairs form, 4 waves of two slots per lane group, has it too)
-            constexpr int kDeep = NW >= 8 || S == 2 ? 2 : 1;
+            constexpr int kDeep = NW >= 8 ? 2 : 1;
             // (user-range classes C > 1: the loop that polls the next range
             // during the current block and publishes every C - 1 positions)
             const bool deep = kDeep == 2 && (p.flags & MF_FLAG_DEEP_PIPE);
@@ -1539,7 +1532,7 @@ struct StrataRun {
             const void* sfn = nullptr;
             size_t slds = 0;
             int32_t cap = std::max(p.max_users, 1);
-            if constexpr (kDeep == 2 && V <= 2 && NW >= 8) {   // (rows of <= 2 vectors per lane)
+            if constexpr (kDeep == 2 && V <= 2) {      // (rows of <= 2 vectors per lane)
                 if ((p.flags & MF_FLAG_STREAM) && deep && a.cls > 1 && p.B <= 256 &&
                     cap <= 4 * TH) {
                     slds = strata_stream_lds_bytes<T>(p.max_items, cap, p.k, TH, p.n_seq) +

@@ -28,7 +28,6 @@ MF_FLAG_L2_HANDOFF = 256
 MF_FLAG_NO_EARLY_POLL = 512
 MF_FLAG_STREAM = 1024
 MF_FLAG_PREPARE = 2048
-MF_FLAG_PAIRS = 4096
 MF_FLAG_CLASSES_SHIFT = 24       # bits 24..27: user-range classes - 1
 MF_STRATA_MAX_CLASSES = 4
 MF_ERR_CAPACITY = 3

@@ -1118,20 +1118,6 @@ class SGDEngine:
             return bool(self.strata_stream)
         return self.STREAM_DEFAULT
 
-    # the pairs form of the 8-wave FP32 k <= 32 kernels (MF_FLAG_PAIRS: 4
-    # waves, two slots per lane group); None = the default, env
-    # MF_STRATA_PAIRS=0/1 overrides
-    strata_pairs: Optional[bool] = None
-    PAIRS_DEFAULT = False
-
-    def _pairs(self) -> bool:
-        env = os.environ.get("MF_STRATA_PAIRS")
-        if env in ("0", "1"):
-            return env == "1"
-        if self.strata_pairs is not None:
-            return bool(self.strata_pairs)
-        return self.PAIRS_DEFAULT
-
     def _deep_pipe(self, pl) -> bool:
         """By the plan: on for plans of few busy slots per step (the 8-wave
         plans, or 16-wave plans filled below 70 %), whose steps wait on the
@@ -1253,8 +1239,6 @@ class SGDEngine:
             flags |= _lib.MF_FLAG_NO_EARLY_POLL
         if pl.narrow:
             flags |= _lib.MF_FLAG_NARROW
-        elif self._pairs():
-            flags |= _lib.MF_FLAG_PAIRS          # (the launcher applies it where it exists)
         flags |= (pl.classes - 1) << _lib.MF_FLAG_CLASSES_SHIFT
         # user rows handed over inside an XCD through its L2 (needs the
         # XCD-class stratum order; the launcher checks the order, the kernel

@@ -203,38 +203,6 @@ def test_deep_pipe_equals_per_stratum_launches(dtype, B, kernel, k, nu, ni, wave
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("kernel,k,B,nu,ni", [
-    ("sigmoid", 32, 8, 3000, 1200),
-    ("sigmoid", 20, 8, 3000, 1200),                  # row tails
-    ("linear", 32, 6, 200, 2000),                    # rows forwarded from t-1 and t-2
-    ("rbf", 28, 7, 3000, 1200),
-])
-def test_pairs_form_equals_per_stratum_launches(kernel, k, B, nu, ni, monkeypatch):
-    """MF_FLAG_PAIRS (the 8-wave FP32 plan of lane groups of 8 run by 4
-    waves, two slots per lane group, user rows two steps ahead) is the same
-    sequential order: bit-identical to the 8-wave persistent sweep and to
-    one launch per stratum, user-only epochs included."""
-    nnz = 150000 if nu > 1000 else 100000
-    u, i, r = _synthetic(71, nu, ni, nnz)
-    rs = np.random.RandomState(72)
-    P = rs.normal(0, 0.1, (nu, k)); Q = rs.normal(0, 0.1, (ni, k))
-    bu = rs.normal(0, 0.1, nu); bi = rs.normal(0, 0.1, ni)
-    out = []
-    for pairs, persistent in (("1", True), ("0", True), ("1", False)):
-        monkeypatch.setenv("MF_STRATA_PAIRS", pairs)
-        eng = _engine(u, i, r, nu, ni, k, kernel, "float32", P, Q, bu, bi)
-        eng.prepare_strata(n_blocks=B, waves=8)
-        for ep in range(3):
-            seq = np.random.RandomState(ep).permutation(B).astype(np.int32)
-            eng.epoch_strata(seq, 3000 + ep, lr=0.01, reg=0.02, update_item=ep != 2,
-                             persistent=persistent)
-        eng.check_strata()
-        out.append(eng.params_numpy())
-    for other in out[1:]:
-        for a, b in zip(out[0], other):
-            assert np.array_equal(a, b)
-
-
 @pytest.mark.parametrize("kernel,k,waves,dtype", [
     ("sigmoid", 32, 8, "float32"), ("linear", 64, 8, "float32"), ("rbf", 16, 8, "float32"),
     ("sigmoid", 32, 4, "float32"), ("linear", 16, 4, "float32"),
