@@ -11,6 +11,10 @@ through size-independent properties where it does not.
       stratum; train RMSE finite and falling over two epochs.  (The full-
       epoch C3 comparison with the oracle, in the GPU's order and in the
       reference's shuffle order, is bench.py's parity leg: ~1 min of CPU.)
+      And the FP64 headline path itself: fit()'s default plan (4 classes,
+      two item phases, two relabelled plans, the stream kernel) for one
+      epoch on the relabelled plan vs the FP64 oracle in its serial order
+      -- parameters max |diff| <= 1e-11 * max(1, |value|), RMSE <= 1e-12.
   C5  1M x 100K, 100M ratings, ALS rank 128: the user half-sweep of the
       first 10K users vs oracle.als_half_sweep -- parameters max relative
       diff <= 2e-4 (f32 MFMA Gramian + f32 solve vs f64).
@@ -92,6 +96,49 @@ def test_c2_shape_strata_vs_oracle():
                 assert err <= 1e-11 * max(1.0, float(np.max(np.abs(b)))), err
             assert abs(rm_g - rm_o) <= 1e-12
         del eng
+
+
+@pytest.mark.timeout(600)
+def test_c3_fp64_default_plan_epoch_equals_oracle(c3_data):
+    """the headline's FP64 path at full C3 size inside
+    the test suite, not only in bench.py's parity leg.  The engine fit()
+    builds (default plan: B = 256, 4 user-range classes, two relabelled
+    plans; the persistent stream kernel) runs one epoch whose rotation seed
+    picks the relabelled plan -- P, Q, b_u, b_i gathered into its
+    labelling, swept, gathered back (mf_permute_rows) -- and the FP64 oracle
+    (oracle/mf_oracle.c) runs the same epoch in eng.serial_order.  ~1 min
+    of one CPU core."""
+    import oracle
+    from matrix_factorization.engine import stratum_order
+
+    u, i, r = c3_data
+    nu, ni, k = 1_000_000, 100_000, 64
+    P0, Q0 = _init(nu, ni, k, np.float32)
+    P0, Q0 = P0.astype(np.float64), Q0.astype(np.float64)
+    eng = _engine(u, i, r, nu, ni, k, "linear", "float64")
+    plan = eng.prepare_strata()
+    assert plan.classes == 4 and len(eng._regroups) == 1
+    eng.load_params(P0, Q0, np.zeros(nu), np.zeros(ni))
+    rs = np.random.RandomState(11)
+    seq = stratum_order(rs, plan)
+    seed = next(s for s in range(1, 1000) if eng._regroup_pick(s) == 1)
+    eng.epoch_strata(seq, seed, 0.01, 0.02)
+    eng.sse_async(0)
+    eng.check_strata()
+    Pg, Qg, bug, big = eng.params_numpy()
+    rm_gpu = eng.rmse_values(1)[0]
+    order = eng.serial_order(seq, seed).astype(np.int64)
+    assert len(order) == len(u)
+    mu = eng.global_mean
+    hyp = dict(kernel="linear", gamma=1.0 / k, min_rating=1.0, max_rating=5.0)
+    P2, Q2, bu2, bi2 = P0.copy(), Q0.copy(), np.zeros(nu), np.zeros(ni)
+    rr = eng.r_host.astype(np.float64)
+    oracle.sgd_pass(eng.u_host, eng.i_host, rr, mu, bu2, bi2, P2, Q2, lr=0.01, reg=0.02,
+                    order=order, **hyp)
+    for a, b in ((Pg, P2), (Qg, Q2), (bug, bu2), (big, bi2)):
+        assert np.max(np.abs(a - b)) <= 1e-11 * max(1.0, float(np.max(np.abs(b))))
+    ro = oracle.rmse(eng.u_host, eng.i_host, rr, mu, bu2, bi2, P2, Q2, **hyp)
+    assert abs(rm_gpu - ro) <= 1e-12
 
 
 def test_c3_shape_persistent_equals_per_stratum(c3_data):
