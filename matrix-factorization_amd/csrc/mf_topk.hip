@@ -1514,14 +1514,25 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
             for (int i = 0; i < 16; ++i) y[i] = 0.f;
             by = bi;
             const bool have = c0 + c < iend;
+            // admission test of tile c's rows between the MFMAs, one branch
+            // per tile (a tile admits anything rarely once the floor is set:
+            // the per-row ballot and branch were most of the loop's issue)
+            bool anyl = false;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
 #pragma unroll
                 for (int m = i * NM / 16; m < (i + 1) * NM / 16; ++m) mfma_m(y, m);
                 if (i == 7) load_half(c0 + 64, 0);       // tile c+2, columns of the first half
                 const float sp = ((A.mu + bx) + ubu[i]) + x[i];
-                const uint64_t bal = __builtin_amdgcn_ballot_w64(have && sp >= uadm[i]);
-                if (bal) insert_row(i, c0, x, bx, bal);  // wave-uniform
+                anyl = anyl || (have && sp >= uadm[i]);
+            }
+            if (__builtin_amdgcn_ballot_w64(anyl)) {     // wave-uniform
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float sp = ((A.mu + bx) + ubu[i]) + x[i];
+                    const uint64_t bal = __builtin_amdgcn_ballot_w64(have && sp >= uadm[i]);
+                    if (bal) insert_row(i, c0, x, bx, bal);
+                }
             }
             load_half(c0 + 64, 1);
             settle();
