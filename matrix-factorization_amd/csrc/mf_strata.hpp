@@ -88,8 +88,6 @@ struct StrataArgs {
     int32_t* xtab;           // nullable: MF_FLAG_L2_HANDOFF -- per workgroup ((base+1) << 4) | XCC id
     int32_t early;           // persistent, C > 1: poll the next position's user range during
                              // the current block (0: MF_FLAG_NO_EARLY_POLL)
-    int32_t nobar;           // probe (MF_STRATA_NOBAR=1, timing only, WRONG results): no
-                             // per-step LDS barrier in strata_block -- what the barrier costs
 };
 
 // first step of block `blk` in this epoch (mirrored by engine.strata_mix)
@@ -312,7 +310,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
             }
             uprev[x] = (rwX.have[x] && A.upd_user) ? rwX.u[x] : -1;
         }
-        if (!A.nobar) lds_barrier();
+        lds_barrier();
     };
 
     // DEPTH 2: the rows applied at step t were gathered at the start of step
@@ -383,7 +381,7 @@ __device__ __forceinline__ void strata_block(const StrataArgs<T>& A, int64_t blk
             uprev2[x] = uprev[x];
             uprev[x] = (Ra.have[x] && A.upd_user) ? Ra.u[x] : -1;
         }
-        if (!A.nobar) lds_barrier();
+        lds_barrier();
     };
 
     Tri ta, tb;
@@ -1501,10 +1499,6 @@ struct StrataRun {
         a.probe = strata_probe_ptr();
         a.xtab = nullptr;
         a.early = (p.flags & MF_FLAG_NO_EARLY_POLL) ? 0 : 1;
-        {
-            const char* nb = std::getenv("MF_STRATA_NOBAR");      // probe: timing only
-            a.nobar = nb && std::atoi(nb) == 1 ? 1 : 0;
-        }
         hipEvent_t ev[2] = {nullptr, nullptr};
         if (p.kernel_ms && !(p.flags & MF_FLAG_PREPARE)) {
             MF_HIP_CHECK(hipEventCreate(&ev[0]));
