@@ -16,10 +16,11 @@ Three keyword arguments are new and default to the reference's behaviour:
               valid sequential order per epoch -- the throughput setting.
               Known deviation: a different order trains to a slightly
               different model.  At C3 (20 epochs) the default strata plan
-              ends +0.36e-5 train RMSE over the mean of the reference's
-              random orders (24 draws, round 5; +0.64e-5 pooled with round
-              4's 48, about 2.7 standard errors), where the reference's own
-              run-to-run spread is ~1e-5; "exact" has no such gap.
+              ends +0.32e-5 train RMSE over the mean of the reference's
+              random orders (24 draws against 28 reference runs, round 5;
+              +0.60e-5 pooled with round 4's 48 draws, about 2.7 standard
+              errors), where the reference's own run-to-run SD is ~1e-5;
+              "exact" has no such gap.
 ``device``    HIP device ("cuda", "cuda:1", ...); None = current device.
 ``distributed`` False (default) or True: process-group mode.  When
               torch.distributed is initialised with world_size > 1, every
