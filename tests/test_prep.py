@@ -47,6 +47,25 @@ def test_legacy_shuffle_mid_stream():
         assert np.array_equal(a, b) and np.array_equal(x1, x2), draws
 
 
+@pytest.mark.parametrize("dtype,n,draws", [(np.int32, 5_000_000, 0), (np.int32, 4_194_305, 623),
+                                           (np.int64, 4_500_001, 624), (np.int32, 6_000_011, 5)])
+def test_large_shuffle_is_numpys(dtype, n, draws):
+    """Millions of elements (the prefetch ring wraps many times, the MT state
+    crosses thousands of 624-word blocks): the same permutation and the same
+    RandomState afterwards as np.random.shuffle, from any MT position."""
+    np.random.seed(19)
+    np.random.randint(0, 10, draws)
+    st = np.random.get_state()
+    a = np.arange(n, dtype=dtype)
+    np.random.shuffle(a)
+    x1 = np.random.rand(3)
+    np.random.set_state(st)
+    b = np.arange(n, dtype=dtype)
+    _prep.legacy_shuffle_(b)
+    x2 = np.random.rand(3)
+    assert np.array_equal(a, b) and np.array_equal(x1, x2)
+
+
 def test_legacy_shuffle_falls_back_for_other_layouts():
     np.random.seed(3)
     a = np.arange(1000, dtype=np.int32)
