@@ -109,31 +109,57 @@ struct MT {
 
 namespace {
 
-// NumPy's _shuffle_raw on x[0..n): swap targets drawn kWin positions ahead of
-// the swap that uses them (the draws do not depend on the data) so the
-// random line is in cache when the swap reaches it.
+inline uint32_t mt_temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+// NumPy's _shuffle_raw on x[0..n): for i = n-1 .. 1, swap x[i] with
+// x[random_interval(i)].  The draws do not depend on the data, so they are
+// made a block of MT outputs at a time, ahead of the swaps that use them
+// (each target prefetched), and without a branch per output: every tempered
+// output is tested against the current draw's bound and the draw index
+// advances by the outcome -- the same outputs consumed, the same rejections
+// as MT::interval, the same MT position afterwards.  (The one-thread draw
+// loop with its ~30 % mispredicted rejection branch was 0.53 of the 0.65 s
+// shuffle of 100M on the GPU box's CPU; tools/shuffle_probe.cpp.)
 template <typename E>
 void shuffle_raw(MT& mt, E* data, int64_t n) {
-    constexpr int kWin = 64;
-    uint32_t ring[kWin];
-    int64_t i = n - 1, drawn = n - 1;  // next swap index / next index to draw for
-    const int64_t pre = std::min<int64_t>(kWin, std::max<int64_t>(n - 1, 0));
-    for (int w = 0; w < pre; ++w, --drawn) {
-        const uint32_t j = mt.interval((uint32_t)drawn);
-        ring[drawn % kWin] = j;
-        __builtin_prefetch(data + j, 1, 1);
-    }
-    for (; i >= 1; --i) {
-        const int64_t j = ring[i % kWin];
-        if (drawn >= 1) {
-            const uint32_t jn = mt.interval((uint32_t)drawn);
-            ring[drawn % kWin] = jn;
-            __builtin_prefetch(data + jn, 1, 1);
-            --drawn;
+    if (n < 2) return;
+    const int64_t total = n - 1;                     // draws, for i = n-1 .. 1
+    constexpr int64_t kR = 2048, kAhead = 64;        // target ring; swaps this far behind
+    uint32_t ring[kR];
+    int64_t drawn = 0, done = 0;
+    while (done < total) {
+        if (drawn < total) {                         // the rest of one MT block
+            if (mt.pos == kN) mt.regen();
+            int p = mt.pos;
+            uint32_t maxv = (uint32_t)(total - drawn);   // bound of draw `drawn`: i = n-1-drawn
+            int64_t d = drawn;
+            while (p < kN) {
+                const uint32_t mask = 0xffffffffu >> __builtin_clz(maxv);   // maxv >= 1
+                const uint32_t v = mt_temper(mt.key[p++]) & mask;
+                const uint32_t acc = v <= maxv ? 1u : 0u;
+                ring[d & (kR - 1)] = v;
+                __builtin_prefetch(data + v, 1, 1);
+                d += acc;
+                maxv -= acc;
+                if (d == total) break;
+            }
+            mt.pos = p;
+            drawn = d;
         }
-        const E t = data[i];
-        data[i] = data[j];
-        data[j] = t;
+        const int64_t lim = drawn < total ? drawn - kAhead : total;
+        for (; done < lim; ++done) {
+            const int64_t i = total - done;
+            const int64_t j = ring[done & (kR - 1)];
+            const E t = data[i];
+            data[i] = data[j];
+            data[j] = t;
+        }
     }
 }
 
