@@ -60,13 +60,12 @@ struct Scratch {
     std::vector<int32_t> sc, ic, path;
 };
 
-// Plan one block: its m ratings (user ids bu[], item ids bi[], rating
-// indices brow[], in row order) with item ids in [ilo, ilo+nqi) and user ids
-// in [ulo, ulo+nus).  Returns D; with `out` (D*NS entries) also writes the
-// grid there (rating index per position, -1 = idle slot).
-int32_t plan_block(const int32_t* bu, const int32_t* bi, const int32_t* brow, int32_t m,
+// Plan one block: its m ratings (user ids bu[], item ids bi[], in row order)
+// with item ids in [ilo, ilo+nqi) and user ids in [ulo, ulo+nus).  Returns D and writes each rating's position in the
+// block's D*NS grid (step * NS + slot) to pos[].
+int32_t plan_block(const int32_t* bu, const int32_t* bi, int32_t m,
                    int32_t ilo, int32_t nqi, int32_t ulo, int32_t nus, int32_t NS, Scratch& S,
-                   int32_t* out) {
+                   int32_t* pos) {
     if (m == 0) return 0;
     using clk = std::chrono::steady_clock;
     const auto c0 = clk::now();
@@ -142,7 +141,6 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, const int32_t* brow, in
         S.ucnt[ul] = 0;
         S.uslot[ul] = -1;
     }
-    if (!out) return D;                          // the step count only
     const auto c2 = clk::now();
     // Koenig edge colouring with D colours
     S.sc.assign((size_t)NS * D, -1);
@@ -226,8 +224,7 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, const int32_t* brow, in
         }
     }
     const auto c3 = clk::now();
-    std::fill(out, out + (size_t)D * NS, -1);
-    for (int32_t e = 0; e < m; ++e) out[(size_t)S.ecol[e] * NS + S.es[e]] = brow[e];
+    for (int32_t e = 0; e < m; ++e) pos[e] = S.ecol[e] * NS + S.es[e];
     const auto c4 = clk::now();
     auto ns = [](auto a, auto b) {
         return (int64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
@@ -376,15 +373,18 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
     strip.reset();
     lap("block pass");
 
-    // Plan the blocks in chunks of 64 on worker threads, twice: the steps of
-    // every block first (slot loads and item degrees: cheap), so the grid has
-    // its final place, then each block coloured straight into it.
+    // Plan the blocks in chunks of 64 on worker threads, in one pass: a
+    // block's step count is known only once it is coloured, so each rating's
+    // grid position (step * NS + slot, < 2^31: D <= m) is kept beside it and
+    // the grids are written once the step offsets are summed -- a scatter
+    // instead of a second planning pass for the steps.
     const int64_t CH = 64;
     const int64_t nch = (BB + CH - 1) / CH;
     std::vector<int32_t> steps(BB, 0);
+    auto b_pos = buf(n);
     const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     const unsigned nt = (unsigned)std::min<int64_t>(hw, std::max<int64_t>(1, n / 200000));
-    auto blocks = [&](bool colour, const int64_t* bstep, int32_t* sched) {
+    {
         std::atomic<int64_t> next{0};
         mf::ThreadErr err;
         auto worker = [&]() { err.guard([&]() {
@@ -397,12 +397,10 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
                     const int32_t sv = (int32_t)(b / B), w = (int32_t)(b % B);
                     const int32_t ub = (int32_t)(((int64_t)sv + (int64_t)C * w) % CB);
                     const int64_t o = boff[b];
-                    const int32_t d = plan_block(
-                        b_u.get() + o, b_i.get() + o, b_row.get() + o, (int32_t)(boff[b + 1] - o),
+                    steps[b] = plan_block(
+                        b_u.get() + o, b_i.get() + o, (int32_t)(boff[b + 1] - o),
                         item_bounds[w], item_bounds[w + 1] - item_bounds[w], user_bounds[ub],
-                        user_bounds[ub + 1] - user_bounds[ub], n_slots, S,
-                        colour ? sched + bstep[b] * n_slots : nullptr);
-                    if (!colour) steps[b] = d;
+                        user_bounds[ub + 1] - user_bounds[ub], n_slots, S, b_pos.get() + o);
                 }
             }
         }); };
@@ -411,9 +409,10 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
         worker();
         for (auto& t : th) t.join();
         err.rethrow();                                 // -> the C ABI's bad_alloc path
-    };
-    blocks(false, nullptr, nullptr);
-    lap("block steps");
+    }
+    b_u.reset();
+    b_i.reset();
+    lap("plan blocks");
 
     auto* plan = new (std::nothrow) mf_strata_plan;
     if (!plan) {
@@ -433,8 +432,15 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
         return MF_ERR_NOMEM;
     }
     plan->n_sched = plan->bstep[BB] * n_slots;
-    blocks(true, plan->bstep.data(), plan->sched.get());
-    lap("plan blocks");
+    int32_t* sched = plan->sched.get();
+    mf::for_buckets((int)nch, T, [&](int c) {
+        for (int64_t b = c * CH; b < std::min(BB, (c + 1) * CH); ++b) {
+            int32_t* grid = sched + plan->bstep[b] * n_slots;
+            std::fill(grid, grid + (int64_t)steps[b] * n_slots, -1);
+            for (int64_t e = boff[b]; e < boff[b + 1]; ++e) grid[b_pos[e]] = b_row[e];
+        }
+    });
+    lap("grids");
     if (tm) {
         std::fprintf(stderr, "[mf_strata_plan]   per-block phases (thread-s): users+sort %.3f, "
                      "slots+edges %.3f, colour %.3f, grid %.3f; repairs %lld, mean path %.1f\n",
