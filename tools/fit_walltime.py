@@ -123,6 +123,25 @@ def main():
     else:
         kmf.fit_epochs = timed("epochs", with_events)
     SGDEngine.prepare_strata = timed("strata_plan", SGDEngine.prepare_strata)
+    # the engine build's parts (no synchronisation: wall time of each call as
+    # the host sees it, summed per function; the regrouping's run on the
+    # worker thread beside the engine's own)
+    import matrix_factorization.engine as eng_mod
+    ecalls = {}
+
+    def timed_e(name, fn):
+        def wrap(*a, **kw):
+            t = time.perf_counter()
+            out = fn(*a, **kw)
+            ecalls[name] = ecalls.get(name, 0.0) + time.perf_counter() - t
+            return out
+        return wrap
+
+    eng_mod.sched_strata = timed_e("sched_strata", eng_mod.sched_strata)
+    eng_mod.StrataPlan.to_device = timed_e("plan_to_device", eng_mod.StrataPlan.to_device)
+    for name in ("_build_regroup", "_regroup_buffers", "_prime_strata", "_ensure_strata_ws",
+                 "_item_phases", "degree_cum", "__init__"):
+        setattr(SGDEngine, name, timed_e(name.strip("_"), getattr(SGDEngine, name)))
     SGDEngine.snapshot_params = timed("start_snapshot", SGDEngine.snapshot_params)
     KernelMF._sync_params = timed("download", KernelMF._sync_params)
     torch.zeros(1, device="cuda:0")
@@ -151,6 +170,7 @@ def main():
                                    "thread while epoch e's levels are built and launched"),
                "phases_s": {k: round(v, 3) for k, v in phases.items()},
                "prep_calls_s": {k: round(v, 3) for k, v in calls.items()},
+               "engine_calls_s": {k: round(v, 3) for k, v in ecalls.items()},
                "final_train_rmse": float(m.train_rmse[-1]),
                "train_rmse": [float(x) for x in m.train_rmse],
                "host_threads": os.environ.get("MF_HOST_THREADS") or min(16, os.cpu_count()),
@@ -190,6 +210,7 @@ def main():
                                       "of both together"),
                       "phases_s": {k: round(v, 3) for k, v in phases.items()},
                       "prep_calls_s": {k: round(v, 3) for k, v in calls.items()},
+                      "engine_calls_s": {k: round(v, 3) for k, v in ecalls.items()},
                       "epoch_ms_events": ep_ms,
                       "epoch_ms_events_note": ("hipEvents between consecutive epochs of "
                                                "fit_epochs (SGD sweep + RMSE pass each); "
