@@ -445,6 +445,35 @@ def test_strata_plan_is_valid(B, NS, C):
                 assert nst == 0
 
 
+def test_strata_plans_are_pinned():
+    """The planner's output (sched + block step offsets) on skewed inputs is
+    the one it had before the one-pass rewrite of round 5 (tools/plan_hash.py:
+    the same sha256 from the two-pass build, here and on the GPU box's host;
+    C3 at full scale is pinned there too).  Any change to the planner that
+    moves a rating shows up here."""
+    import hashlib
+
+    from matrix_factorization import engine as E
+
+    want = ["4e332a691e1ae04ad6782bf0ae7301f64c2cb4f38f703cf6dce9819863f05c25",
+            "a150593315c716afb5c326d8874e69025f626ba8b2767d77a4d674dce57b4609",
+            "6eecfc3dd146cb5c5d8065c4684ed33ee1794b5d87bee70acbef2ff4bd6a0269",
+            "607bf684bd7297f2a93fe1367c79178d662f2881b0fe59f48e734a31fd337fd3"]
+    rng = np.random.default_rng(7)
+    got = []
+    for (nu, ni, n, B, C, ns) in [(500, 300, 20000, 8, 1, 64), (500, 300, 20000, 8, 3, 32),
+                                  (40000, 9000, 600000, 32, 4, 128),
+                                  (40000, 9000, 600000, 48, 2, 256)]:
+        u = rng.integers(0, nu, n).astype(np.int32)
+        i = np.minimum((rng.pareto(1.2, n) * 50).astype(np.int64), ni - 1).astype(np.int32)
+        sched, bstep = E.sched_strata(u, i, nu, ni, B, E.balanced_bounds(u, nu, C * B),
+                                      E.balanced_bounds(i, ni, B), ns, C)
+        h = hashlib.sha256(sched.tobytes())
+        h.update(bstep.tobytes())
+        got.append(h.hexdigest())
+    assert got == want
+
+
 def test_strata_serial_order_and_rejections():
     from matrix_factorization import _lib
     from matrix_factorization import engine as E
