@@ -601,6 +601,18 @@ int mf_strata_plan_build_classes(const int32_t* user_ids, const int32_t* item_id
                                  int32_t n_classes, const int32_t* user_bounds,
                                  const int32_t* item_bounds, int32_t n_slots,
                                  mf_strata_plan** plan_out);
+/* mf_strata_plan_build_classes over n_cands (slots, waves) kernel shapes
+ * (1..8): the step counts of each (no colouring) pick the shape of least
+ * steps * waves (ties: the earlier one), the first one outright when its plan
+ * fills at least fill_stop of its positions (n / (steps * slots); 0 = never);
+ * only the pick is planned in full.  *picked = its index.  The plan is the
+ * one mf_strata_plan_build_classes builds with that shape's slot count. */
+int mf_strata_plan_build_pick(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
+                              int32_t n_users, int32_t n_items, int32_t n_blocks,
+                              int32_t n_classes, const int32_t* user_bounds,
+                              const int32_t* item_bounds, const int32_t* slot_cands,
+                              const int32_t* wave_cands, int32_t n_cands, double fill_stop,
+                              int32_t* picked, mf_strata_plan** plan_out);
 int mf_strata_plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
                          int32_t n_users, int32_t n_items, int32_t n_blocks,
                          const int32_t* user_bounds, const int32_t* item_bounds,

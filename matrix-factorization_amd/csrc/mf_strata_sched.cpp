@@ -61,14 +61,33 @@ struct Scratch {
 };
 
 // Plan one block: its m ratings (user ids bu[], item ids bi[], in row order)
-// with item ids in [ilo, ilo+nqi) and user ids in [ulo, ulo+nus).  Returns D and writes each rating's position in the
-// block's D*NS grid (step * NS + slot) to pos[].
+// with item ids in [ilo, ilo+nqi) and user ids in [ulo, ulo+nus).  Returns D
+// and, with `pos`, writes each rating's position in the block's D*NS grid
+// (step * NS + slot) to pos[] (without: the step count only -- D is known
+// before the colouring).  es_save: each rating's slot is written there;
+// es_load: the slots are taken from there (a step-count pass of the same NS)
+// instead of being assigned again.
 int32_t plan_block(const int32_t* bu, const int32_t* bi, int32_t m,
                    int32_t ilo, int32_t nqi, int32_t ulo, int32_t nus, int32_t NS, Scratch& S,
-                   int32_t* pos) {
+                   int32_t* pos, int32_t* es_save = nullptr, const int32_t* es_load = nullptr) {
     if (m == 0) return 0;
     using clk = std::chrono::steady_clock;
     const auto c0 = clk::now();
+    auto c1 = c0;
+    int32_t D = 1;
+    if (es_load) {                               // slots known: loads and degrees only
+        S.es.assign(es_load, es_load + m);
+        S.eq.resize(m);
+        S.icnt.assign(nqi, 0);
+        S.load.assign(NS, 0);
+        for (int32_t x = 0; x < m; ++x) {
+            S.eq[x] = bi[x] - ilo;
+            D = std::max(D, ++S.icnt[S.eq[x]]);
+            D = std::max(D, ++S.load[S.es[x]]);
+        }
+        goto colour;
+    }
+    {
     if ((int32_t)S.ucnt.size() < nus) {
         S.ucnt.resize(nus, 0);
         S.uslot.resize(nus, -1);
@@ -93,7 +112,7 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, int32_t m,
         for (int32_t ul = 0; ul < nus; ++ul)
             if (S.ucnt[ul] > 0) S.order[(size_t)S.dstart[maxdeg - S.ucnt[ul]]++] = ul;
     }
-    const auto c1 = clk::now();
+    c1 = clk::now();
     // each user onto the least loaded slot, ties to the lowest slot index
     // (the order a (load, slot) min-heap pops): one bit set of slots per load
     // level, the lowest set bit of the lowest non-empty level is the slot
@@ -105,7 +124,7 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, int32_t m,
     S.lvl.assign((size_t)cap * WD, 0);
     for (int32_t x = 0; x < NS; ++x) S.lvl[(size_t)(x >> 6)] |= 1ull << (x & 63);
     S.load.assign(NS, 0);
-    int32_t D = 1, low = 0;
+    int32_t low = 0;
     for (int32_t ul : S.order) {
         while (true) {                                            // lowest non-empty level
             bool any = false;
@@ -141,6 +160,10 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, int32_t m,
         S.ucnt[ul] = 0;
         S.uslot[ul] = -1;
     }
+    if (es_save) std::copy(S.es.begin(), S.es.begin() + m, es_save);
+    }
+    if (!pos) return D;                          // the step count only
+colour:
     const auto c2 = clk::now();
     // Koenig edge colouring with D colours
     S.sc.assign((size_t)NS * D, -1);
@@ -247,18 +270,26 @@ bool bounds_ok(const int32_t* b, int32_t nb, int32_t total) {
 
 static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
                       int32_t n_users, int32_t n_items, int32_t n_blocks, int32_t n_classes,
-                      const int32_t* user_bounds, const int32_t* item_bounds, int32_t n_slots,
-                      mf_strata_plan** plan_out) {
+                      const int32_t* user_bounds, const int32_t* item_bounds,
+                      const int32_t* slot_cands, const int32_t* wave_cands, int32_t n_cands,
+                      double fill_stop, int32_t* picked, mf_strata_plan** plan_out) {
     if (!plan_out) {
         set_error("NULL plan_out");
         return MF_ERR_INVALID;
     }
     *plan_out = nullptr;
-    if (n < 0 || n_users < 0 || n_items < 0 || n_blocks < 1 || n_slots < 1 || n_slots > 4096 ||
-        n_classes < 1 || n_classes > MF_STRATA_MAX_CLASSES) {
-        set_error("invalid sizes (n=%lld, n_blocks=%d, n_classes=%d, n_slots=%d)", (long long)n,
-                  n_blocks, n_classes, n_slots);
+    if (!slot_cands || !wave_cands || n_cands < 1 || n_cands > 8) {
+        set_error("1 to 8 (slots, waves) candidates expected");
         return MF_ERR_INVALID;
+    }
+    for (int32_t c = 0; c < n_cands; ++c) {
+        if (n < 0 || n_users < 0 || n_items < 0 || n_blocks < 1 || slot_cands[c] < 1 ||
+            slot_cands[c] > 4096 || wave_cands[c] < 1 || n_classes < 1 ||
+            n_classes > MF_STRATA_MAX_CLASSES) {
+            set_error("invalid sizes (n=%lld, n_blocks=%d, n_classes=%d, n_slots=%d, waves=%d)",
+                      (long long)n, n_blocks, n_classes, slot_cands[c], wave_cands[c]);
+            return MF_ERR_INVALID;
+        }
     }
     if ((int64_t)n_classes * n_blocks * n_blocks >= ((int64_t)1 << 31) || n > INT32_MAX) {
         set_error("n_blocks=%d / n=%lld too large", n_blocks, (long long)n);
@@ -373,18 +404,21 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
     strip.reset();
     lap("block pass");
 
-    // Plan the blocks in chunks of 64 on worker threads, in one pass: a
-    // block's step count is known only once it is coloured, so each rating's
-    // grid position (step * NS + slot, < 2^31: D <= m) is kept beside it and
-    // the grids are written once the step offsets are summed -- a scatter
-    // instead of a second planning pass for the steps.
+    // Plan the blocks in chunks of 64 on worker threads.  With several
+    // (slots, waves) candidates, the step counts of each come first (the slot
+    // assignment and the degrees: no colouring) and pick the one of least
+    // steps * waves -- the first as soon as it fills fill_stop of its
+    // positions; then the pick is planned in one pass: a block's step count
+    // is known only once it is coloured, so each rating's grid position
+    // (step * NS + slot, < 2^31: D <= m) is kept beside it and the grids are
+    // written once the step offsets are summed.
     const int64_t CH = 64;
     const int64_t nch = (BB + CH - 1) / CH;
     std::vector<int32_t> steps(BB, 0);
     auto b_pos = buf(n);
     const unsigned hw = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     const unsigned nt = (unsigned)std::min<int64_t>(hw, std::max<int64_t>(1, n / 200000));
-    {
+    auto blocks = [&](int32_t NS, int32_t* pos, int32_t* es_save, const int32_t* es_load) {
         std::atomic<int64_t> next{0};
         mf::ThreadErr err;
         auto worker = [&]() { err.guard([&]() {
@@ -400,7 +434,8 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
                     steps[b] = plan_block(
                         b_u.get() + o, b_i.get() + o, (int32_t)(boff[b + 1] - o),
                         item_bounds[w], item_bounds[w + 1] - item_bounds[w], user_bounds[ub],
-                        user_bounds[ub + 1] - user_bounds[ub], n_slots, S, b_pos.get() + o);
+                        user_bounds[ub + 1] - user_bounds[ub], NS, S, pos ? pos + o : nullptr,
+                        es_save ? es_save + o : nullptr, es_load ? es_load + o : nullptr);
                 }
             }
         }); };
@@ -409,7 +444,35 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
         worker();
         for (auto& t : th) t.join();
         err.rethrow();                                 // -> the C ABI's bad_alloc path
+    };
+    int32_t pick = 0;
+    // the slots of the best candidate so far and of the current one: the
+    // pick's full pass colours from them instead of assigning them again
+    decltype(buf(0)) es_best, es_cur;
+    if (n_cands > 1) {
+        int64_t best = -1;
+        es_best = buf(n);
+        es_cur = buf(n);
+        for (int32_t c = 0; c < n_cands; ++c) {
+            blocks(slot_cands[c], nullptr, es_cur.get(), nullptr);
+            int64_t total = 0;
+            for (int64_t b = 0; b < BB; ++b) total += steps[b];
+            const int64_t cost = total * wave_cands[c];
+            if (best < 0 || cost < best) {
+                best = cost;
+                pick = c;
+                std::swap(es_best, es_cur);
+            }
+            const double fill = (double)n / (double)std::max<int64_t>(total * slot_cands[c], 1);
+            if (c == 0 && fill_stop > 0 && fill >= fill_stop) break;
+        }
+        lap("candidate steps");
     }
+    const int32_t n_slots = slot_cands[pick];
+    if (picked) *picked = pick;
+    es_cur.reset();
+    blocks(n_slots, b_pos.get(), nullptr, es_best ? es_best.get() : nullptr);
+    es_best.reset();
     b_u.reset();
     b_i.reset();
     lap("plan blocks");
@@ -455,6 +518,28 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
     return MF_OK;
 }
 
+extern "C" int mf_strata_plan_build_pick(const int32_t* user_ids, const int32_t* item_ids,
+                                         int64_t n, int32_t n_users, int32_t n_items,
+                                         int32_t n_blocks, int32_t n_classes,
+                                         const int32_t* user_bounds, const int32_t* item_bounds,
+                                         const int32_t* slot_cands, const int32_t* wave_cands,
+                                         int32_t n_cands, double fill_stop, int32_t* picked,
+                                         mf_strata_plan** plan_out) {
+    try {
+        return plan_build(user_ids, item_ids, n, n_users, n_items, n_blocks, n_classes,
+                          user_bounds, item_bounds, slot_cands, wave_cands, n_cands, fill_stop,
+                          picked, plan_out);
+    } catch (const std::bad_alloc&) {
+        if (plan_out) *plan_out = nullptr;
+        set_error("out of host memory (strata plan of %lld ratings)", (long long)n);
+        return MF_ERR_NOMEM;
+    } catch (const std::exception& e) {
+        if (plan_out) *plan_out = nullptr;
+        set_error("strata planner failed: %s", e.what());
+        return MF_ERR_INVALID;
+    }
+}
+
 extern "C" int mf_strata_plan_build_classes(const int32_t* user_ids, const int32_t* item_ids,
                                             int64_t n, int32_t n_users, int32_t n_items,
                                             int32_t n_blocks, int32_t n_classes,
@@ -462,8 +547,9 @@ extern "C" int mf_strata_plan_build_classes(const int32_t* user_ids, const int32
                                             const int32_t* item_bounds, int32_t n_slots,
                                             mf_strata_plan** plan_out) {
     try {
+        const int32_t waves = 1;
         return plan_build(user_ids, item_ids, n, n_users, n_items, n_blocks, n_classes,
-                          user_bounds, item_bounds, n_slots, plan_out);
+                          user_bounds, item_bounds, &n_slots, &waves, 1, 0.0, nullptr, plan_out);
     } catch (const std::bad_alloc&) {
         if (plan_out) *plan_out = nullptr;
         set_error("out of host memory (strata plan of %lld ratings)", (long long)n);

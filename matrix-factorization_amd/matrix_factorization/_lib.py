@@ -121,6 +121,8 @@ SIGNATURES = {
         _P, _P, _I64, _I32, _I32, _I32, _P, _P, _I32, _P]),
     "mf_strata_plan_build_classes": (ctypes.c_int, [
         _P, _P, _I64, _I32, _I32, _I32, _I32, _P, _P, _I32, _P]),
+    "mf_strata_plan_build_pick": (ctypes.c_int, [
+        _P, _P, _I64, _I32, _I32, _I32, _I32, _P, _P, _P, _P, _I32, ctypes.c_double, _P, _P]),
     "mf_strata_plan_positions": (_I64, [_P]),
     "mf_strata_plan_fetch": (ctypes.c_int, [_P, _P, _P]),
     "mf_strata_plan_free": (None, [_P]),

@@ -360,6 +360,37 @@ def sched_strata(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int, n_blo
     return sched[:npos], bstep
 
 
+def sched_strata_pick(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int, n_blocks: int,
+                      ubnd: np.ndarray, ibnd: np.ndarray, shapes, classes: int = 1,
+                      fill_stop: float = 0.0):
+    """mf_strata_plan_build_pick + fetch: (sched, block step offsets, index
+    of the picked (slots, waves) shape) -- the plan ``sched_strata`` builds
+    with the slots of the shape of least steps * waves (the first outright
+    when it fills ``fill_stop`` of its positions); the other shapes' step
+    counts come without their colouring."""
+    n = len(u)
+    u = np.ascontiguousarray(u, np.int32)
+    i = np.ascontiguousarray(i, np.int32)
+    ubnd = np.ascontiguousarray(ubnd, np.int32)
+    ibnd = np.ascontiguousarray(ibnd, np.int32)
+    slots = np.ascontiguousarray([s for s, _ in shapes], np.int32)
+    waves = np.ascontiguousarray([w for _, w in shapes], np.int32)
+    lib = _lib.load()
+    handle = ctypes.c_void_p()
+    picked = ctypes.c_int32(-1)
+    _lib.call("mf_strata_plan_build_pick", _np(u), _np(i), n, n_users, n_items, n_blocks,
+              int(classes), _np(ubnd), _np(ibnd), _np(slots), _np(waves), len(shapes),
+              float(fill_stop), ctypes.byref(picked), ctypes.byref(handle))
+    try:
+        npos = int(lib.mf_strata_plan_positions(handle))
+        sched = np.empty(max(npos, 1), np.int32)
+        bstep = np.empty(int(classes) * n_blocks * n_blocks + 1, np.int64)
+        _lib.call("mf_strata_plan_fetch", handle, _np(sched), _np(bstep))
+    finally:
+        lib.mf_strata_plan_free(handle)
+    return sched[:npos], bstep, int(picked.value)
+
+
 def strata_slots(k: int, dcode: int, waves: int = 16) -> int:
     """Rating slots per step of the strata kernel with ``waves`` waves per
     workgroup (16, or 8 for FP32 rows of k <= 64); 0 if that kernel does not
@@ -1031,9 +1062,8 @@ class SGDEngine:
                                                    self.k, self.dcode)
             if need > _lib.load().mf_strata_lds_limit():
                 ib = balanced_bounds(i, n_items, B, False)   # equal item counts
-        n = len(u)
         cand = [waves] if waves is not None else [16, 8]
-        best = None
+        shapes = []
         for wv in cand:
             ns = strata_slots(self.k, self.dcode, wv)
             if ns <= 0:
@@ -1041,13 +1071,16 @@ class SGDEngine:
                     raise ValueError(f"no {wv}-wave strata kernel for n_factors={self.k}, "
                                      f"dtype={self.dtype}")
                 continue
-            sched, bstep = sched_strata(u, i, self.n_users, n_items, B, ub, ib, ns, classes)
-            cost = int(bstep[-1]) * wv
-            if best is None or cost < best[0]:
-                best = (cost, ns, sched, bstep)
-            if waves is None and wv == 16 and n / max(len(sched), 1) >= 0.7:
-                break                       # well filled: the 16-wave plan it is
-        _, ns, sched, bstep = best
+            shapes.append((ns, wv))
+        if not shapes:
+            raise ValueError(f"no strata kernel for n_factors={self.k}, dtype={self.dtype}")
+        # the shape of least steps * waves (the per-CU VALU issue of an epoch);
+        # the 16-wave plan outright when it fills 70 % of its positions.  Only
+        # the pick is coloured (mf_strata_plan_build_pick)
+        fill_stop = 0.7 if waves is None and shapes[0][1] == 16 else 0.0
+        sched, bstep, j = sched_strata_pick(u, i, self.n_users, n_items, B, ub, ib, shapes,
+                                            classes, fill_stop)
+        ns = shapes[j][0]
         plan = StrataPlan(B, ns, ub, ib, bstep, sched, classes)
         plan.narrow = waves == 4
         return plan

@@ -474,6 +474,44 @@ def test_strata_plans_are_pinned():
     assert got == want
 
 
+@pytest.mark.parametrize("n,shapes", [(20000, [(128, 16), (64, 8)]), (20000, [(64, 16), (32, 8)]),
+                                      (200000, [(128, 16), (64, 8)]),
+                                      (200000, [(64, 16), (32, 8)]), (3000, [(64, 16)]),
+                                      (-400000, [(64, 16), (32, 8)]),
+                                      (-400000, [(128, 16), (64, 8)])])
+def test_strata_plan_pick_is_the_rule_over_full_plans(n, shapes):
+    """mf_strata_plan_build_pick (step counts without colouring, only the pick
+    coloured) returns the shape and the plan that building every shape in
+    full and keeping the least steps * waves returns (the 16-wave one
+    outright at >= 70 % fill) -- SGDEngine._build_plan's rule before."""
+    from matrix_factorization import engine as E
+
+    # n < 0: |n| ratings in 4 x 4 dense blocks of uniform items (plans of
+    # >= 70 % fill, so the 16-wave shape is taken outright); else skewed
+    # items in 16 x 8 sparse blocks
+    rng = np.random.default_rng(abs(n) + len(shapes) + shapes[0][0])
+    dense, n = n < 0, abs(n)
+    nu, ni, B, C = (3000, 2000, 4, 1) if dense else (3000, 2000, 8, 2)
+    u = rng.integers(0, nu, n).astype(np.int32)
+    i = (rng.integers(0, ni, n) if dense else
+         np.minimum((rng.pareto(1.5, n) * 200).astype(np.int64), ni - 1)).astype(np.int32)
+    ub, ib = E.balanced_bounds(u, nu, C * B), E.balanced_bounds(i, ni, B)
+    for fill_stop in (0.7, 0.0):
+        best = None
+        for j, (ns, wv) in enumerate(shapes):
+            sched, bstep = E.sched_strata(u, i, nu, ni, B, ub, ib, ns, C)
+            cost = int(bstep[-1]) * wv
+            if best is None or cost < best[0]:
+                best = (cost, j, sched, bstep)
+            if j == 0 and fill_stop and n / max(len(sched), 1) >= fill_stop:
+                break
+        sched, bstep, j = E.sched_strata_pick(u, i, nu, ni, B, ub, ib, shapes, C, fill_stop)
+        if dense and fill_stop:
+            assert j == 0 and n / len(sched) >= fill_stop
+        assert j == best[1]
+        assert np.array_equal(sched, best[2]) and np.array_equal(bstep, best[3])
+
+
 def test_strata_serial_order_and_rejections():
     from matrix_factorization import _lib
     from matrix_factorization import engine as E

@@ -128,19 +128,26 @@ def main():
     # worker thread beside the engine's own)
     import matrix_factorization.engine as eng_mod
     ecalls = {}
+    timeline = []                    # (name, thread, start, end), seconds from fit()'s start
+    import threading
 
     def timed_e(name, fn):
         def wrap(*a, **kw):
             t = time.perf_counter()
             out = fn(*a, **kw)
-            ecalls[name] = ecalls.get(name, 0.0) + time.perf_counter() - t
+            t1 = time.perf_counter()
+            ecalls[name] = ecalls.get(name, 0.0) + t1 - t
+            timeline.append((name, threading.current_thread().name, t, t1))
             return out
         return wrap
 
     eng_mod.sched_strata = timed_e("sched_strata", eng_mod.sched_strata)
+    eng_mod.sched_slices = timed_e("sched_slices", eng_mod.sched_slices)
+    for name in ("normal",):
+        setattr(np.random, name, timed_e(name, getattr(np.random, name)))
     eng_mod.StrataPlan.to_device = timed_e("plan_to_device", eng_mod.StrataPlan.to_device)
     for name in ("_build_regroup", "_regroup_buffers", "_prime_strata", "_ensure_strata_ws",
-                 "_item_phases", "degree_cum", "__init__"):
+                 "_item_phases", "degree_cum", "__init__", "_upload_triples", "_build_eval"):
         setattr(SGDEngine, name, timed_e(name.strip("_"), getattr(SGDEngine, name)))
     SGDEngine.snapshot_params = timed("start_snapshot", SGDEngine.snapshot_params)
     KernelMF._sync_params = timed("download", KernelMF._sync_params)
@@ -171,6 +178,7 @@ def main():
                "phases_s": {k: round(v, 3) for k, v in phases.items()},
                "prep_calls_s": {k: round(v, 3) for k, v in calls.items()},
                "engine_calls_s": {k: round(v, 3) for k, v in ecalls.items()},
+               "engine_timeline_s": [(a, b, round(c - t, 3), round(d - t, 3)) for a, b, c, d in timeline],
                "final_train_rmse": float(m.train_rmse[-1]),
                "train_rmse": [float(x) for x in m.train_rmse],
                "host_threads": os.environ.get("MF_HOST_THREADS") or min(16, os.cpu_count()),
@@ -211,6 +219,7 @@ def main():
                       "phases_s": {k: round(v, 3) for k, v in phases.items()},
                       "prep_calls_s": {k: round(v, 3) for k, v in calls.items()},
                       "engine_calls_s": {k: round(v, 3) for k, v in ecalls.items()},
+               "engine_timeline_s": [(a, b, round(c - t, 3), round(d - t, 3)) for a, b, c, d in timeline],
                       "epoch_ms_events": ep_ms,
                       "epoch_ms_events_note": ("hipEvents between consecutive epochs of "
                                                "fit_epochs (SGD sweep + RMSE pass each); "
