@@ -80,6 +80,31 @@ WORKLOADS = {
 }
 
 
+def record_maps_at_exit() -> None:
+    """With MF_MAPS_DIR set (tools/gpu.sh sets it per step): this process's
+    library map, written by a Python atexit hook -- the last Python code
+    before the C exit handlers (HIP's fat-binary unregistration of each
+    code object, torch's allocator teardown, rocprofv3's tool finalisation)
+    run, so the PCs of a fault there (the r05n abort)
+    can be matched to a library.  tools/gpu.sh deletes the file when the
+    step exits 0."""
+    d = os.environ.get("MF_MAPS_DIR")
+    if not d:
+        return
+    import atexit
+
+    def dump():
+        try:
+            os.makedirs(d, exist_ok=True)
+            with open("/proc/self/maps") as f, open(os.path.join(d, f"maps.{os.getpid()}.txt"),
+                                                     "w") as g:
+                g.write(f.read())
+        except OSError:
+            pass
+
+    atexit.register(dump)
+
+
 def log(msg: str) -> None:
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
@@ -247,6 +272,7 @@ def run_als(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
                    "step": "one ALS epoch: user half-sweep + item half-sweep + training RMSE"},
         "final_rmse": rmse[-1], "rmse_per_epoch": rmse, "roofline": roofline,
         "phases": phases, "cpu_baseline": cpu_baseline, "parity": parity,
+        "launch": _launch_label(),
     }
     print(json.dumps(out), flush=True)
     return 0
@@ -376,9 +402,15 @@ def run_topk(args, u, i, r, nu, ni, nnz, k, desc, mu, P0, Q0, dev) -> int:
                    "chunk_users": batch["chunk"], "path": path},
         "roofline": roof,
         "cpu_baseline": cpu_baseline, "parity": parity,
+        "launch": _launch_label(),
     }
     print(json.dumps(out), flush=True)
     return 0
+
+
+def _launch_label() -> str:
+    from matrix_factorization.engine import launch_form_label
+    return launch_form_label()
 
 
 def host_info() -> dict:
@@ -791,6 +823,7 @@ def main() -> int:
                     help="N>1 process group: nccl (= RCCL, one GPU per rank) or gloo "
                          "(rehearsal: ranks may share a GPU, LOCAL_RANK mod device count)")
     args = ap.parse_args()
+    record_maps_at_exit()
 
     import torch
     import torch.distributed as dist
@@ -858,7 +891,8 @@ def main() -> int:
 def nested_line(o: dict) -> dict:
     """The FP32 perf-layout run, nested under the FP64 headline line."""
     keep = ("value", "unit", "ms_per_step", "dtype", "final_rmse", "rmse_per_epoch",
-            "roofline", "phases", "parity", "multi_gpu", "projection", "schedule_build_s")
+            "roofline", "phases", "parity", "multi_gpu", "projection", "schedule_build_s",
+            "launch")
     d = {kk: o.get(kk) for kk in keep if kk in o}
     d["schedule"] = o["config"]["schedule"]
     d["arithmetic"] = ("FP32 parameters; fused multiply-adds, v_exp_f32 / v_rcp_f32 "
@@ -878,7 +912,8 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
                                                   any_rank_failed, global_rmse, item_ranges,
                                                   local_shard, rotation_epoch,
                                                   rotation_final_ranges, shard_users)
-    from matrix_factorization.engine import SGDEngine, strata_slots
+    from matrix_factorization.engine import (STREAM_MAX_STEPS, SGDEngine, launch_form_label,
+                                             max_block_steps, strata_slots)
 
     args = argparse.Namespace(**{**vars(args), "dtype": dtype})
     P0, Q0 = P0.astype(dtype), Q0.astype(dtype)
@@ -1138,7 +1173,7 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
             alg = alg_epoch * len(events)                           # algorithmic bytes
             achieved = alg / sgd_s / 1e9
             stream = (strata and persistent and cls > 1 and eng._deep_pipe(plan)
-                      and eng._stream())
+                      and eng._stream() and max_block_steps(plan) <= STREAM_MAX_STEPS)
             kname = ((("k_sgd_strata_stream" if stream else "k_sgd_strata_epoch")
                       if persistent else "k_sgd_strata") if strata else "k_sgd_batch")
             traffic = traffic_from_profiles(args.workload, world, args.schedule
@@ -1206,6 +1241,9 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
             "roofline": roofline, "phases": phases,
             "cpu_baseline": cpu_baseline, "parity": parity, "multi_gpu": multi,
             "schedule_build_s": t_sched,
+            # how the persistent sweeps were launched in this process: plain
+            # under rocprofv3's preload (engine._under_rocprofiler)
+            "launch": launch_form_label(),
         }
         if emu > 1:
             emulation_fields(args, out, elapsed, emu, nnz, dev, u, i, r, nu, ni, k, kernel, mu,

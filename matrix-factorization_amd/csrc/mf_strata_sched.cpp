@@ -26,6 +26,7 @@
 #include <functional>
 #include <memory>
 #include <new>
+#include <stdexcept>
 #include <thread>
 #include <vector>
 
@@ -164,6 +165,10 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, int32_t m,
     }
     if (!pos) return D;                          // the step count only
 colour:
+    // a grid position is step * NS + slot in int32: a block whose D x NS grid
+    // reaches 2^31 (one very skewed block: D can reach m) is refused
+    if ((int64_t)D * NS >= ((int64_t)1 << 31))
+        throw std::length_error("a strata block's grid of D x NS positions reaches 2^31");
     const auto c2 = clk::now();
     // Koenig edge colouring with D colours
     S.sc.assign((size_t)NS * D, -1);

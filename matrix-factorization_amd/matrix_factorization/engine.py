@@ -555,12 +555,49 @@ def stratum_order(rs, nb, mode: Optional[str] = None, classes: Optional[int] = N
 
 
 def _under_rocprofiler() -> bool:
-    """True inside `rocprofv3 ... -- python ...`: its dispatch interception
-    (ROCm 7.x) segfaults on hipLaunchCooperativeKernel, so profiled runs
-    launch the persistent strata kernel plainly (same kernel; the occupancy
-    check stays the co-residency guard)."""
-    return ("rocprofiler" in os.environ.get("LD_PRELOAD", "")
-            or any(k.startswith("ROCPROF") for k in os.environ))
+    """True when rocprofv3's tool library is preloaded into this process
+    (`rocprofv3 ... -- python ...` puts librocprofiler-sdk-tool in
+    LD_PRELOAD).  Profiled runs then launch the persistent strata kernel
+    plainly -- the same kernel; the occupancy check stays the co-residency
+    guard -- and bench.py labels its line "launch": "plain (profiler)".
+    Why ("the r05n abort"): one profiled top-k bench
+    exited 139 in its C exit handlers after its JSON line was out; nothing
+    ties that fault to the cooperative launch, so this is caution, kept
+    narrow: only the preload counts, not any ROCPROF* variable in the
+    environment (MF_PROFILER_PLAIN=0 turns it off)."""
+    if os.environ.get("MF_PROFILER_PLAIN") == "0":
+        return False
+    return "librocprofiler" in os.environ.get("LD_PRELOAD", "")
+
+
+def launch_form_label() -> str:
+    """How the persistent sweeps are launched in this process (bench.py's
+    line carries it)."""
+    if os.environ.get("MF_STRATA_COOP") == "0":
+        return "plain (MF_STRATA_COOP=0)"
+    return "plain (profiler)" if _under_rocprofiler() else "cooperative"
+
+
+# the stream kernel's per-position step count is a 16-bit field
+STREAM_MAX_STEPS = 0xFFFF
+
+
+def max_block_steps(pl) -> int:
+    """Largest number of steps of one block over every phase of a plan."""
+    cached = getattr(pl, "_max_block_steps", None)
+    if cached is not None:
+        return cached
+    subs = pl.phases if hasattr(pl, "phases") else [pl]
+    m = 0
+    for sub in subs:
+        bs = np.asarray(sub.bstep)
+        if bs.size > 1:
+            m = max(m, int(np.diff(bs).max()))
+    try:
+        pl._max_block_steps = m
+    except AttributeError:
+        pass
+    return m
 
 
 def default_sgd_flags() -> int:
@@ -1264,7 +1301,10 @@ class SGDEngine:
         flags = _lib.MF_FLAG_PERSISTENT if persistent else 0
         if persistent and self._deep_pipe(pl):
             flags |= _lib.MF_FLAG_DEEP_PIPE
-            if pl.classes > 1 and self._stream():
+            # the stream kernel keeps a block's step count in a 16-bit field
+            # of its LDS geometry table: a plan with a longer block runs the
+            # per-block form (same order, bit for bit)
+            if pl.classes > 1 and self._stream() and max_block_steps(pl) <= STREAM_MAX_STEPS:
                 flags |= _lib.MF_FLAG_STREAM
         if os.environ.get("MF_STRATA_COOP") == "0" or _under_rocprofiler():
             flags |= _lib.MF_FLAG_NO_COOP
@@ -1410,30 +1450,34 @@ class SGDEngine:
         threads (sched_levels_chunked, the same bits as the greedy levels)
         straight into one of two pinned buffers, uploaded asynchronously on
         the launch stream (the host builds epoch e+1's levels while the GPU
-        still runs epoch e; a buffer is rewritten only once its last upload
-        has completed)."""
+        still runs epoch e).  Host AND device schedules are double-buffered:
+        pair k is rewritten only once the event recorded after epoch k's
+        level launches has completed, so a caller that switches streams
+        between epochs cannot overwrite a schedule still being read."""
         st = getattr(self, "_exact_bufs", None)
         if st is None or st["host"][0].numel() < self.n:
             st = {"host": [torch.empty(self.n, dtype=torch.int32, pin_memory=True)
                            for _ in range(2)],
                   "ev": [None, None], "flip": 0,
-                  "dev": torch.empty(self.n, dtype=torch.int32, device=self.dev)}
+                  "dev": [torch.empty(self.n, dtype=torch.int32, device=self.dev)
+                          for _ in range(2)]}
             self._exact_bufs = st
         k = st["flip"]
         st["flip"] ^= 1
         if st["ev"][k] is not None:
             st["ev"][k].synchronize()
-        hb = st["host"][k]
+        hb, db = st["host"][k], st["dev"][k]
         _, offs = sched_levels_chunked(self.u_host, self.i_host, order, self.n_users,
                                        self.n_items, update_user, update_item,
                                        out=hb.numpy())
         with torch.cuda.device(self.dev):
             stream = torch.cuda.current_stream(self.dev)
-            st["dev"][: self.n].copy_(hb[: self.n], non_blocking=True)
+            db[: self.n].copy_(hb[: self.n], non_blocking=True)
+            out = self._run(db, offs, None, lr, reg, update_user, update_item, 0, timing)
             ev = torch.cuda.Event()
-            ev.record(stream)
+            ev.record(stream)           # after the upload AND the launches reading db
             st["ev"][k] = ev
-        return self._run(st["dev"], offs, None, lr, reg, update_user, update_item, 0, timing)
+        return out
 
     def epoch_colored(self, seq: Optional[np.ndarray], lr: float, reg: float,
                       update_user: bool = True, update_item: bool = True,
@@ -1907,44 +1951,49 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
             engine.epoch_strata(sq, sd, lr, reg, update_user, update_item, persistent=False)
             engine.sse_async(ep)
 
-    for epoch in range(n_epochs):
-        if poll is not None and persistent is None and poll.failed():
-            replay_failed(epoch)                  # stop launching persistent sweeps now
-        if schedule == "exact":
-            if exact_next is not None:            # drawn during the last epoch
-                spare, order = order, exact_next.result()
-                exact_spare, exact_next = spare, None
+    try:
+        for epoch in range(n_epochs):
+            if poll is not None and persistent is None and poll.failed():
+                replay_failed(epoch)                  # stop launching persistent sweeps now
+            if schedule == "exact":
+                if exact_next is not None:            # drawn during the last epoch
+                    spare, order = order, exact_next.result()
+                    exact_spare, exact_next = spare, None
+                else:
+                    _prep.legacy_shuffle_(order)      # = np.random.shuffle(order)
+                if pipeline and epoch + 1 < n_epochs:
+                    exact_next = exact_pool.submit(shuffled_copy, order, exact_spare)
+                try:
+                    engine.epoch_exact(order, lr, reg, update_user, update_item)
+                finally:
+                    if exact_next is not None:
+                        exact_next.exception()        # joined: RNG consistent at the epoch end
+            elif schedule == "colored":
+                seq = np.random.permutation(nb).astype(np.int32)
+                engine.epoch_colored(seq, lr, reg, update_user, update_item)
             else:
-                _prep.legacy_shuffle_(order)      # = np.random.shuffle(order)
-            if pipeline and epoch + 1 < n_epochs:
-                exact_next = exact_pool.submit(shuffled_copy, order, exact_spare)
-            try:
-                engine.epoch_exact(order, lr, reg, update_user, update_item)
-            finally:
-                if exact_next is not None:
-                    exact_next.exception()        # joined: RNG consistent at the epoch end
-        elif schedule == "colored":
-            seq = np.random.permutation(nb).astype(np.int32)
-            engine.epoch_colored(seq, lr, reg, update_user, update_item)
-        else:
-            seq = stratum_order(np.random, engine.strata)
-            seed = int(np.random.randint(0, 2**31 - 1))
-            draws.append((seq, seed))
-            engine.epoch_strata(seq, seed, lr, reg, update_user, update_item,
-                                persistent=persistent)
-            if poll is not None and persistent is None:
-                poll.post()
-        engine.sse_async(epoch)
-        if verbose == 1:
-            if snap0 is not None and persistent is None and engine.strata_failed():
-                replay_failed(epoch + 1)
-            rmse = engine.rmse_values(epoch + 1)[epoch]
-            train_rmse.append(rmse)
-            print("Epoch ", epoch + 1, "/", n_epochs, " -  train_rmse:", rmse)
-        if on_epoch is not None:
-            on_epoch(epoch)
-    if schedule == "exact" and pipeline:
-        exact_pool.shutdown()
+                seq = stratum_order(np.random, engine.strata)
+                seed = int(np.random.randint(0, 2**31 - 1))
+                draws.append((seq, seed))
+                engine.epoch_strata(seq, seed, lr, reg, update_user, update_item,
+                                    persistent=persistent)
+                if poll is not None and persistent is None:
+                    poll.post()
+            engine.sse_async(epoch)
+            if verbose == 1:
+                if snap0 is not None and persistent is None and engine.strata_failed():
+                    replay_failed(epoch + 1)
+                rmse = engine.rmse_values(epoch + 1)[epoch]
+                train_rmse.append(rmse)
+                print("Epoch ", epoch + 1, "/", n_epochs, " -  train_rmse:", rmse)
+            if on_epoch is not None:
+                on_epoch(epoch)
+    finally:
+        # also on an exception mid-fit: the worker is joined and dropped (a
+        # fit aborted in the exact schedule leaves the global RandomState
+        # one shuffle past the reference's: epoch e+1's was already drawn)
+        if schedule == "exact" and pipeline:
+            exact_pool.shutdown(wait=True, cancel_futures=True)
     if snap0 is not None and persistent is None and engine.strata_failed():
         replay_failed(n_epochs)
         if verbose == 1:

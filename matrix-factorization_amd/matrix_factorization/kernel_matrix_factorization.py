@@ -26,9 +26,13 @@ Three keyword arguments are new and default to the reference's behaviour:
               torch.distributed is initialised with world_size > 1, every
               rank calls ``fit`` with the same data and the same NumPy RNG
               state; users are sharded across the ranks (one GPU each,
-              RCCL all-reduce of the item-row deltas once per epoch,
               distributed.fit_sharded) and every rank ends with the full
-              model.  Needs schedule "strata" or "colored".
+              model.  How the ranks share the item rows is ``exchange``
+              below: by default ("rotate") each rank holds one item range
+              at a time and passes it round the ring (RCCL send / recv)
+              between N sub-epochs, then one all-gather; "delta" is the
+              once-per-epoch all-reduce of the item-row deltas.  Needs
+              schedule "strata" or "colored".
 ``strata_classes``  schedule "strata" only: user-range classes of the plan,
               "auto" (default: 4 for the linear kernel where an item meets
               >= 2 ratings per user range and block, else 1 -- the order

@@ -634,6 +634,80 @@ def test_deep_pipe_default_by_plan_shape(monkeypatch):
     assert deep(plan(ns16, 1100)) is True
 
 
+def test_stream_form_gated_on_block_steps(monkeypatch):
+    """MF_FLAG_STREAM only for plans whose every block fits the stream
+    kernel's 16-bit step field: one oversized block of one item
+    phase sends the whole plan to the per-block form."""
+    from types import SimpleNamespace
+
+    from matrix_factorization import _lib
+    from matrix_factorization.engine import STREAM_MAX_STEPS, SGDEngine, max_block_steps
+
+    for v in ("MF_STRATA_STREAM", "MF_STRATA_DEEP", "MF_STRATA_COOP", "MF_STRATA_L2",
+              "MF_STRATA_EARLY", "MF_PROFILER_PLAIN"):
+        monkeypatch.delenv(v, raising=False)
+    monkeypatch.setenv("LD_PRELOAD", "")
+    eng = SimpleNamespace(strata_persistent=True, strata_deep_pipe=True, strata_stream=None,
+                          STREAM_DEFAULT=True)
+    eng._deep_pipe = lambda pl: SGDEngine._deep_pipe(eng, pl)
+    eng._stream = lambda: SGDEngine._stream(eng)
+
+    def plan(steps_per_block, phases=1):
+        subs = [SimpleNamespace(bstep=np.concatenate([[0], np.cumsum(s)]).astype(np.int64))
+                for s in steps_per_block]
+        pl = SimpleNamespace(classes=4, narrow=False, l2_handoff=False)
+        if phases > 1:
+            pl.phases = subs
+        else:
+            pl.bstep = subs[0].bstep
+        return pl
+
+    ok = plan([[3, 9, STREAM_MAX_STEPS]])
+    big = plan([[3, 9, 12], [4, STREAM_MAX_STEPS + 1]], phases=2)
+    assert max_block_steps(ok) == STREAM_MAX_STEPS
+    assert max_block_steps(big) == STREAM_MAX_STEPS + 1
+    flags = lambda pl: SGDEngine._strata_flags(eng, pl, True)  # noqa: E731
+    assert flags(ok) & _lib.MF_FLAG_STREAM
+    assert not flags(big) & _lib.MF_FLAG_STREAM
+    assert flags(big) & _lib.MF_FLAG_DEEP_PIPE             # the per-block form, still deep
+
+
+def test_profiler_detection_is_the_preload_only(monkeypatch):
+    """Persistent sweeps launch plainly only under rocprofv3's preloaded tool
+    library, not because some ROCPROF* variable is set."""
+    from matrix_factorization.engine import _under_rocprofiler, launch_form_label
+
+    monkeypatch.delenv("MF_PROFILER_PLAIN", raising=False)
+    monkeypatch.delenv("MF_STRATA_COOP", raising=False)
+    monkeypatch.setenv("LD_PRELOAD", "")
+    monkeypatch.setenv("ROCPROFILER_SOMETHING", "1")
+    assert not _under_rocprofiler() and launch_form_label() == "cooperative"
+    monkeypatch.setenv("LD_PRELOAD", "/opt/rocm/lib/rocprofiler-sdk/librocprofiler-sdk-tool.so")
+    assert _under_rocprofiler() and launch_form_label() == "plain (profiler)"
+    monkeypatch.setenv("MF_PROFILER_PLAIN", "0")
+    assert not _under_rocprofiler()
+
+
+def test_strata_planner_refuses_int32_grid_overflow():
+    """A block whose D x NS grid reaches 2^31 positions is refused with an
+    error instead of wrapping the int32 grid index: one item
+    rated by 600K users is a block of D = 600K steps; at 4096 slots that is
+    2.46e9 positions."""
+    from matrix_factorization import _lib
+    from matrix_factorization.engine import sched_strata
+
+    m = 600_000
+    u = np.arange(m, dtype=np.int32)
+    i = np.zeros(m, dtype=np.int32)
+    ub = np.array([0, m], np.int32)
+    ib = np.array([0, 1], np.int32)
+    with pytest.raises(_lib.MFLibraryError, match="2\\^31"):
+        sched_strata(u, i, m, 1, 1, ub, ib, 4096)
+    sched, bstep = sched_strata(u[:1000], i[:1000], 1000, 1, 1, np.array([0, 1000], np.int32),
+                                ib, 4096)                 # 1000 x 4096: fine
+    assert int(bstep[-1]) == 1000
+
+
 def test_bench_traffic_lookup_is_keyed_on_world_and_emulation():
     """bench.py's roofline.traffic comes from PMC counters of exactly the
     configuration measured: an --emulate-rank N line must not borrow the

@@ -37,6 +37,9 @@ for step in "$@"; do
     [[ "$step" == *:* ]] && rest=${step#*:}
     args=${rest//,/ }
     p="$O/$(printf %02d $n)_$kind"
+    # bench.py writes its library map here at exit (record_maps_at_exit): kept
+    # only when the step fails, so a fault's PCs can be matched to a library
+    export MF_MAPS_DIR="$p.maps"
     echo "[gpu.sh $(date +%H:%M:%S)] step $n: $step"
     case $kind in
     test)
@@ -89,5 +92,6 @@ for step in "$@"; do
     *)
         echo "unknown step $step" >&2; exit 2 ;;
     esac
+    rm -rf "$p.maps"          # reached only when the step exited 0 (set -e)
 done
 echo "[gpu.sh $(date +%H:%M:%S)] done"
