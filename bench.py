@@ -634,7 +634,8 @@ def multi_checks(args, eng, rotate, world, rank, dev, u, i, r, nu, ni, k, kernel
         if rotate:
             log("check: one-GPU replay of the N-rank rotation order")
             rp = RotationReplay(u, i, r, nu, ni, world, k, kernel, args.dtype, dev,
-                                n_blocks=args.blocks, waves=args.waves, **hyp)
+                                n_blocks=args.blocks, waves=args.waves, relabel=args.relabel,
+                                **hyp)
             rp.load(P0, Q0, np.zeros(nu), np.zeros(ni))
             sse = []
             for ep in range(n_ep):
@@ -799,6 +800,11 @@ def main() -> int:
                     help="N > 1 (strata): rotate = item ranges passed round the ring "
                          "between N sub-epochs (exact: a sequential order, DESIGN.md 6); "
                          "delta = item deltas all-reduced once per epoch, applied damped")
+    ap.add_argument("--no-delta-leg", action="store_true",
+                    help="N > 1, --exchange rotate: skip the nested delta-exchange run")
+    ap.add_argument("--relabel", type=int, default=None,
+                    help="N > 1, --exchange rotate: item relabellings, one drawn per epoch "
+                         "(default distributed.ROTATE_RELABEL = 8; 1 = the plain rotation)")
     ap.add_argument("--delta-scale", type=float, default=None,
                     help="N > 1, --exchange delta: weight of the all-reduced item deltas "
                          "(default min(1/2, 2/N), distributed.default_delta_scale; "
@@ -824,6 +830,9 @@ def main() -> int:
                          "(rehearsal: ranks may share a GPU, LOCAL_RANK mod device count)")
     args = ap.parse_args()
     record_maps_at_exit()
+    if args.relabel is None:
+        from matrix_factorization.distributed import ROTATE_RELABEL
+        args.relabel = ROTATE_RELABEL
 
     import torch
     import torch.distributed as dist
@@ -877,10 +886,23 @@ def main() -> int:
         outs.append(run_sgd(args, dt, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc,
                             mu, P0, Q0, shared))
         torch.cuda.empty_cache()
+    # N > 1, rotate: the other exchange measured in the same job and nested
+    # (`delta_exchange`), so one N-GPU run maps both ends of the frontier
+    # (exact order vs damped item deltas)
+    delta_leg = None
+    if (world > 1 and args.exchange == "rotate" and args.schedule == "strata"
+            and not args.no_delta_leg):
+        log(f"---- {dtypes[0]} run, exchange delta (nested leg)")
+        da = argparse.Namespace(**{**vars(args), "exchange": "delta"})
+        delta_leg = run_sgd(da, dtypes[0], world, rank, dev, u, i, r, nu, ni, nnz, k, kernel,
+                            desc, mu, P0, Q0, shared)
+        torch.cuda.empty_cache()
     if rank == 0:
         out = outs[0]
         if len(outs) > 1:
             out["fp32_layout"] = nested_line(outs[1])
+        if delta_leg is not None:
+            out["delta_exchange"] = nested_line(delta_leg, fp32=False)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -888,16 +910,20 @@ def main() -> int:
     return 0
 
 
-def nested_line(o: dict) -> dict:
-    """The FP32 perf-layout run, nested under the FP64 headline line."""
+def nested_line(o: dict, fp32: bool = True) -> dict:
+    """A second run nested under the headline line: the FP32 perf layout
+    (``fp32``), or at N > 1 the other exchange."""
     keep = ("value", "unit", "ms_per_step", "dtype", "final_rmse", "rmse_per_epoch",
             "roofline", "phases", "parity", "multi_gpu", "projection", "schedule_build_s",
             "launch")
     d = {kk: o.get(kk) for kk in keep if kk in o}
     d["schedule"] = o["config"]["schedule"]
-    d["arithmetic"] = ("FP32 parameters; fused multiply-adds, v_exp_f32 / v_rcp_f32 "
-                       "(DESIGN.md section 3): not the reference's expression order, "
-                       "parity as a tolerance vs the FP64 oracle")
+    d["exchange"] = o["config"].get("exchange")
+    d["item_delta_scale"] = o["config"].get("item_delta_scale")
+    if fp32:
+        d["arithmetic"] = ("FP32 parameters; fused multiply-adds, v_exp_f32 / v_rcp_f32 "
+                           "(DESIGN.md section 3): not the reference's expression order, "
+                           "parity as a tolerance vs the FP64 oracle")
     return d
 
 
@@ -908,10 +934,9 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
     import torch
     import torch.distributed as dist
 
-    from matrix_factorization.distributed import (ReplicaExchange, RotationExchange,
+    from matrix_factorization.distributed import (ReplicaExchange, RotationSet,
                                                   any_rank_failed, global_rmse, item_ranges,
-                                                  local_shard, rotation_epoch,
-                                                  rotation_final_ranges, shard_users)
+                                                  local_shard, shard_users)
     from matrix_factorization.engine import (STREAM_MAX_STEPS, SGDEngine, launch_form_label,
                                              max_block_steps, strata_slots)
 
@@ -976,14 +1001,28 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
     log(f"rank {rank}: {n_local} local ratings, {sched_desc}, scheduled in {t_sched:.1f}s")
     exch = (ReplicaExchange(eng, scale=args.delta_scale) if world > 1 and not rotate
             else None)
-    # rotate: epoch e's gather + RMSE pass on a side stream beside epoch e+1
-    if rotate and emu > 1:
-        rot = _emulated_ring_cls()(eng, ilo, emu, overlap=not args.rotate_no_overlap)
-    else:
-        rot = (RotationExchange(eng, ilo, overlap=not args.rotate_no_overlap) if rotate
-               else None)
+    # rotate: epoch e's gather + RMSE pass on a side stream beside epoch e+1,
+    # over args.relabel item relabellings (one drawn per epoch; RotationSet)
+    rot = None
+    if rotate:
+        t1 = time.time()
+        mk = None
+        if emu > 1:
+            ring = _emulated_ring_cls()
+            mk = lambda e, lo: ring(e, lo, emu, overlap=not args.rotate_no_overlap)  # noqa: E731
+        rot = RotationSet(eng, i, max(world, emu), args.relabel,
+                          overlap=not args.rotate_no_overlap, make_exchange=mk,
+                          prepare=dict(n_blocks=args.blocks, waves=args.waves))
+        if rot.K > 1:
+            sched_desc = sched_desc.replace(
+                "item ranges passed round the ring",
+                f"item ranges passed round the ring, {rot.K} item relabellings, one drawn "
+                f"per epoch")
+        t_sched += time.time() - t1
     rot_overlap = rotate and rot.overlap
     eng._ensure_sse_slots(args.warmup + args.steps + 1)
+    if rot is not None:
+        rot.ensure_sse_slots(args.warmup + args.steps + 1)
 
     def reset_params():
         eng.load_params(P=P_local, bu=np.zeros(n_users_local))
@@ -991,6 +1030,8 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
             exch.bind(Q0, np.zeros(ni))
         else:
             eng.load_params(Q=Q0, bi=np.zeros(ni))
+        if rot is not None:
+            rot.bind()
 
     def seq_for(ep):
         return strata_seq(ep, plan if strata else nb)
@@ -1004,10 +1045,9 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
         the whole rotation epoch, hand-offs and final all-gather included)."""
         if rotate:
             launches = [] if timing else None
-            rotation_epoch(eng, rot, rot_for(ep), args.lr, args.reg, events=events,
-                           launches=launches, epoch=ep,
-                           sse_slot=ep if rot_overlap else None,
-                           sse_timing=events is not None)
+            rot.epoch(rot_for(ep), args.lr, args.reg, events=events, launches=launches,
+                      epoch=ep, sse_slot=ep if rot_overlap else None,
+                      sse_timing=events is not None)
             return (None, sum(launches)) if timing else None
         if strata:
             delta = None if exch is None else (exch.dq, exch.dbi)
@@ -1056,6 +1096,11 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
 
     rot_events = []   # rotate: per timed epoch, the (kind, start, end) events of its parts
 
+    def sse_now(ep):
+        # rotate: the SSE of the labelling the epoch ran in (its engine's
+        # ratings carry that labelling's item ids; shared SSE buffer)
+        (eng if rot is None else rot.engines[rot.cur]).sse_async(ep)
+
     def epoch(ep, timed):
         # hipEvents on the stream the kernels run on (torch's current stream,
         # which the engine launches on): one pair around the epoch's SGD
@@ -1079,7 +1124,7 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
         if overlap:
             eng.sse_overlap(ep, timing=bool(ev))
         elif not rot_overlap:                # rotate + overlap: ran on the side stream
-            eng.sse_async(ep)
+            sse_now(ep)
         if ev:
             ev[3].record()
             events.append(ev)
@@ -1092,7 +1137,7 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
             _, n_launch = run(ep, seq_for(ep), timing=True)
             end()
             if not rot_overlap:
-                eng.sse_async(ep)
+                sse_now(ep)
             persistent = n_launch == n_phases
             if persistent:           # one persistent launch per epoch (per item phase)
                 sched_desc = sched_desc.replace(
@@ -1120,13 +1165,12 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    if strata and any_rank_failed(eng):  # every rank raises together: nobody left waiting
+    if strata and any_rank_failed(eng if rot is None else rot):   # all ranks raise together
         raise SystemExit("a persistent strata sweep gave up waiting (workgroups not "
                          "co-resident): the timed epochs are invalid")
     n_ep = args.warmup + args.steps
-    if rot_overlap:           # the live replica whole again (for the checks), SSEs landed
-        rot.gather(rotation_final_ranges(n_ep - 1, rot.world))
-        rot.join()
+    if rot is not None:       # the live canonical replica whole again (checks), SSEs landed
+        rot.finish(n_ep - 1)
     rmse = global_rmse(eng, n_ep, nnz)
     multi = None
     if world > 1:
@@ -1163,12 +1207,12 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
             exch_s = sum(e[1].elapsed_time(e[2]) for e in events) / 1e3
             sse_s = sum(e[2].elapsed_time(e[3]) for e in events) / 1e3
             if rotate:      # split the rotation epoch into its sweeps and hand-offs
-                part = {"sgd": 0.0, "pass": 0.0, "gather": 0.0}
+                part = {"sgd": 0.0, "pass": 0.0, "gather": 0.0, "relabel": 0.0}
                 for evs in rot_events:
                     for kind, a, b in evs:
                         part[kind] += a.elapsed_time(b) / 1e3
                 sgd_s = part["sgd"]
-                exch_s = part["pass"] + part["gather"]
+                exch_s = part["pass"] + part["gather"] + part["relabel"]
             launches = launches_per_epoch * len(events)
             alg = alg_epoch * len(events)                           # algorithmic bytes
             achieved = alg / sgd_s / 1e9
@@ -1209,6 +1253,7 @@ def run_sgd(args, dtype, world, rank, dev, u, i, r, nu, ni, nnz, k, kernel, desc
                 if rotate:
                     phases["ring_pass_ms_per_epoch"] = part["pass"] / len(events) * 1e3
                     phases["gather_ms_per_epoch"] = part["gather"] / len(events) * 1e3
+                    phases["relabel_ms_per_epoch"] = part["relabel"] / len(events) * 1e3
                 if rot_overlap:
                     side = rot.sse_events[-len(events):]
                     phases["rmse_ms_per_epoch"] = (sum(a.elapsed_time(b) for a, b in side)

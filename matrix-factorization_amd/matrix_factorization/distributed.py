@@ -327,10 +327,12 @@ class RotationExchange:
         """Every rank's final range (rank r holds c_final[r]) into every rank's
         live replica."""
         if self.world == 1:
+            self._whole = "live"
             return
         self.join()
         self._pack(c_final[self.rank])
         self._all_gather_unpack(c_final, None, None, skip_own=True)
+        self._whole = "live"
 
     def snapshot_sse(self, c_final: list, slot: int, sse_blocks: int, timing: bool = False):
         """Epoch end in overlap mode (class docstring): snapshots on the
@@ -363,6 +365,8 @@ class RotationExchange:
                 ev[0].record(side)
             if self.world > 1:
                 self._all_gather_unpack(c_final, ov["Q"], ov["bi"], skip_own=True)
+            gathered = torch.cuda.Event()
+            gathered.record(side)
             e.sse_from(slot, ov["P"], ov["Q"], ov["bu"], ov["bi"], ov["ws"], side, sse_blocks)
             if timing:
                 ev[1].record(side)
@@ -370,6 +374,18 @@ class RotationExchange:
         done = torch.cuda.Event()
         done.record(side)
         ov["done"] = done
+        ov["gathered"] = gathered
+        self._whole = "snapshot"
+
+    def whole_replica(self):
+        """(Q, b_i, event or None): the whole current replica after the last
+        epoch -- the live one if the epoch ended with ``gather``, else the
+        snapshot of ``snapshot_sse`` with the event after its all-gather on
+        the side stream (wait on it before reading; the RMSE pass reads the
+        same snapshot meanwhile, read-only)."""
+        if getattr(self, "_whole", None) == "snapshot":
+            return self._ov["Q"], self._ov["bi"], self._ov["gathered"]
+        return self.e.Q, self.e.bi, None
 
     def join(self) -> None:
         """Make the launch stream wait for the side stream's last pass."""
@@ -438,6 +454,211 @@ def rotation_final_ranges(epoch: int, world: int) -> list:
     return [rotation_range(r, off, world - 1, world) for r in range(world)]
 
 
+# ------------------------------------------------- relabelled item ranges
+# The rotation over K item relabellings (the frontier's
+# "rotrel8"): which items share a range -- and so
+# meet a user shard's ratings in the same burst -- changes from epoch to
+# epoch.  Relabelling q renames canonical item x to perms[q][x]; its item
+# ranges are contiguous ranges of the NEW ids, balanced over all ratings
+# (identical on every rank), and each rank sweeps them with an engine over
+# its ratings in the new ids.  Measured on one GPU (8 virtual ranks, 8 draws,
+# 20 epochs at C3, profiles/r05/frontier_c4_rotation_family_r05o.json): RMSE
+# gap to the reference order +1.69e-3 -> +1.40e-3 at the same sweep time.
+ROTATE_RELABEL = 8
+RELABEL_SEED = 5150           # relabelling q >= 1: RandomState(RELABEL_SEED + q)
+
+
+def item_relabellings(n_items: int, k: int) -> list:
+    """K item relabellings: None (the identity) and K - 1 permutations,
+    perms[q][x] = new id of canonical item x.  Drawn from their own
+    RandomStates, never the global one (the fit's draws stay one integer per
+    epoch)."""
+    return [None] + [np.random.RandomState(RELABEL_SEED + q).permutation(n_items)
+                     for q in range(1, int(k))]
+
+
+def relabel_pick(draw: int, k: int) -> int:
+    """The relabelling of the epoch with ``draw`` (same on every rank)."""
+    if k <= 1:
+        return 0
+    return int(np.random.RandomState([int(draw) & 0x7FFFFFFF, 77]).randint(0, k))
+
+
+def relabel_ranges(item_ids: np.ndarray, n_items: int, world: int, perm) -> np.ndarray:
+    """item_ranges over the relabelled ids of ALL ratings (``item_ids``:
+    canonical ids of every rating of the job)."""
+    ids = item_ids if perm is None else perm[item_ids].astype(np.int32)
+    return item_ranges(ids, n_items, world)
+
+
+def _moves(perms: list, dev):
+    """Per relabelling: (new id of canonical x, canonical id of new y) as
+    device index tensors (None for the identity)."""
+    out = []
+    for p in perms:
+        if p is None:
+            out.append((None, None))
+            continue
+        inv = np.empty_like(p)
+        inv[p] = np.arange(len(p))
+        out.append((torch.as_tensor(p, dtype=torch.int64, device=dev),
+                    torch.as_tensor(inv, dtype=torch.int64, device=dev)))
+    return out
+
+
+def relabel_rows(src: torch.Tensor, dst: torch.Tensor, moves, p: int, q: int) -> None:
+    """dst (rows in labelling q) = src (rows in labelling p), exact copies:
+    dst[y] = src[perm_p[inv_q[y]]]."""
+    fwd_p, _ = moves[p]
+    _, inv_q = moves[q]
+    if inv_q is None and fwd_p is None:
+        dst.copy_(src)
+        return
+    if inv_q is None:
+        idx = fwd_p
+    elif fwd_p is None:
+        idx = inv_q
+    else:
+        idx = fwd_p.index_select(0, inv_q)
+    torch.index_select(src, 0, idx.to(src.device), out=dst)
+
+
+class RotationSet:
+    """This rank's rotation over K item relabellings.
+
+    ``engine`` (canonical item ids) is relabelling 0; relabelling q >= 1 gets
+    an engine over the same ratings with item ids perms[q][i], its own plan
+    over its own item ranges and its own item replica, sharing P / b_u (and
+    the SSE buffer) with ``engine``.  Each epoch runs in the relabelling its
+    draw picks (relabel_pick): when that differs from the last epoch's, the
+    whole current replica -- the snapshot the overlapped RMSE pass all-gathered,
+    or the live one -- is copied into the new labelling first (one device
+    index copy; the main stream waits only for that all-gather, not for the
+    RMSE pass).  ``finish`` gathers the last epoch's ranges and leaves the
+    canonical replica in ``engine``'s Q / b_i.  ``relabel=1`` is the plain
+    rotation (bit for bit the previous product path)."""
+
+    def __init__(self, engine, item_ids: np.ndarray, world: int, relabel: int = ROTATE_RELABEL,
+                 group=None, overlap: bool = False, prepare: Optional[dict] = None,
+                 make_exchange=None, make_engine=None):
+        self.main = engine
+        self.world = int(world)
+        self.K = max(1, int(relabel))
+        n_items = engine.n_items
+        prepare = dict(prepare or {})
+        self.perms = item_relabellings(n_items, self.K)
+        self.ilo = [relabel_ranges(item_ids, n_items, self.world, p) for p in self.perms]
+        mk_ex = make_exchange or (lambda e, ilo: RotationExchange(e, ilo, group, overlap=overlap))
+        self.engines = [engine]
+        if engine.strata is None:
+            engine.prepare_strata(item_bounds=self.ilo[0], **prepare)
+        make = make_engine or SGDEngine
+        for q in range(1, self.K):
+            p = self.perms[q]
+            e = make(engine.u_host, p[engine.i_host].astype(np.int32), engine.r_host,
+                     engine.n_users, n_items, engine.k, getattr(engine, "kernel", "linear"),
+                     getattr(engine, "dtype", "float64"), getattr(engine, "dev", None),
+                     gamma=getattr(engine, "gamma", 0.0),
+                     min_rating=getattr(engine, "min_rating", 0.0),
+                     max_rating=getattr(engine, "max_rating", 5.0),
+                     global_mean=engine.global_mean)
+            e.prepare_strata(item_bounds=self.ilo[q], **prepare)
+            self.engines.append(e)
+        self.rots = [mk_ex(e, ilo) for e, ilo in zip(self.engines, self.ilo)]
+        self.overlap = self.rots[0].overlap
+        self.moves = _moves(self.perms, getattr(engine, "dev", torch.device("cpu")))
+        self.cur = 0                    # labelling the replica is in
+        self.fresh = True               # the current labelling's live replica is whole
+        self.B = engine.strata.B
+        self.sse_events = []            # (start, end) of each timed side-stream RMSE pass
+
+    # ---- parameters
+    def bind(self) -> None:
+        """Point every relabelled engine at the main engine's P / b_u and SSE
+        buffer, give it an item replica of its own, and start from the main
+        engine's (canonical, whole) replica."""
+        m = self.main
+        for e in self.engines[1:]:
+            e.P, e.bu = m.P, m.bu
+            if e.Q is None or e.Q.shape != m.Q.shape or e.Q.dtype != m.Q.dtype:
+                e.Q, e.bi = torch.empty_like(m.Q), torch.empty_like(m.bi)
+            e.sse_buf = m.sse_buf
+        self.cur, self.fresh = 0, True
+
+    def ensure_sse_slots(self, n: int) -> None:
+        self.main._ensure_sse_slots(n)
+        for e in self.engines[1:]:
+            e.sse_buf = self.main.sse_buf
+
+    def _to(self, q: int, timed=None) -> None:
+        """Move the whole current replica into labelling q."""
+        p = self.cur
+        if q == p:
+            return
+        if self.fresh:
+            srcQ, srcb, ev = self.engines[p].Q, self.engines[p].bi, None
+        else:
+            srcQ, srcb, ev = self.rots[p].whole_replica()
+        dst = self.engines[q]
+        dev = getattr(self.main, "dev", torch.device("cpu"))
+        if ev is not None:
+            torch.cuda.current_stream(dev).wait_event(ev)
+        relabel_rows(srcQ, dst.Q, self.moves, p, q)
+        relabel_rows(srcb, dst.bi, self.moves, p, q)
+        self.cur, self.fresh = q, True
+
+    # ---- epochs
+    def epoch(self, draw: int, lr: float, reg: float, update_user: bool = True,
+              update_item: bool = True, events=None, persistent: Optional[bool] = None,
+              launches: Optional[list] = None, epoch: int = 0, sse_slot: Optional[int] = None,
+              sse_timing: bool = False) -> int:
+        """One rotation epoch in the relabelling ``draw`` picks; returns it."""
+        q = relabel_pick(draw, self.K)
+        if q != self.cur:
+            if events is None:
+                self._to(q)
+            else:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                self._to(q)
+                e1.record()
+                events.append(("relabel", e0, e1))
+        rot = self.rots[q]
+        rotation_epoch(self.engines[q], rot, draw, lr, reg, update_user, update_item,
+                       events=events, persistent=persistent, launches=launches, epoch=epoch,
+                       sse_slot=sse_slot, sse_timing=sse_timing)
+        # rotation_epoch ends with rot.gather (live replica whole) or with the
+        # snapshot form (live replica current on this rank's range only)
+        self.fresh = not (rot.overlap and sse_slot is not None)
+        if sse_timing and rot.overlap and sse_slot is not None and rot.sse_events:
+            self.sse_events.append(rot.sse_events[-1])
+        return q
+
+    def finish(self, last_epoch: int) -> None:
+        """The whole replica live on every rank, in canonical ids (main engine)."""
+        q = self.cur
+        self.rots[q].gather(rotation_final_ranges(last_epoch, self.world))
+        self.fresh = True
+        self._to(0)
+        self.join()
+
+    def join(self) -> None:
+        for rot in self.rots:
+            rot.join()
+
+    def failed(self) -> bool:
+        return any(e.strata is not None and e.strata_failed() for e in self.engines)
+
+    def clear_strata_error(self) -> None:
+        for e in self.engines:
+            e.clear_strata_error()
+
+    def reset(self) -> None:
+        """After restoring the main engine's (canonical) parameters."""
+        self.join()
+        self.cur, self.fresh = 0, True
+
+
 class RotationReplay:
     """The N-rank rotation schedule on ONE GPU (rehearsal and check).
 
@@ -447,53 +668,107 @@ class RotationReplay:
     sub-blocks of a sub-epoch are disjoint in users and items, so this is bit
     for bit what N GPUs compute (the kernel's arithmetic depends only on the
     plan, the draws and the values), and each rank's sub-epoch time is
-    measured alone.  ``serial_order`` lists the epoch's sequential order for
-    the oracle."""
+    measured alone.  With ``relabel`` K > 1 (the product default,
+    ROTATE_RELABEL) each epoch runs in the item relabelling its draw picks,
+    as RotationSet does on every rank: one engine set per relabelling, built
+    when first drawn, the shared replica copied into the drawn labelling.
+    ``serial_order`` lists the epoch's sequential order for the oracle."""
 
     def __init__(self, u, i, r, n_users: int, n_items: int, world: int, n_factors: int,
                  kernel: str, dtype: str, device, gamma: float = 0.0, min_rating: float = 0.0,
                  max_rating: float = 5.0, global_mean: float = 0.0,
                  n_blocks: Optional[int] = None, waves: Optional[int] = None, engine_cls=None,
-                 classes: Optional[int] = None):
-        make = SGDEngine if engine_cls is None else engine_cls
+                 classes: Optional[int] = None, relabel: int = ROTATE_RELABEL):
+        self._make = SGDEngine if engine_cls is None else engine_cls
         self.world = world
         self.bounds = shard_users(u, n_users, world)
-        self.ilo = item_ranges(i, n_items, world)
         self.n_items, self.n = n_items, len(u)
-        self.engines, self.gidx = [], []
+        self._data = (u, i, r, n_factors, kernel, dtype, device,
+                      dict(gamma=gamma, min_rating=min_rating, max_rating=max_rating,
+                           global_mean=global_mean))
+        self._prep = dict(n_blocks=n_blocks, classes=classes)
+        if waves is not None:
+            self._prep["waves"] = waves
+        self.K = max(1, int(relabel))
+        self.perms = item_relabellings(n_items, self.K)
+        self.gidx = []
         for rank in range(world):
             lo, hi = int(self.bounds[rank]), int(self.bounds[rank + 1])
-            m = (u >= lo) & (u < hi)
-            self.gidx.append(np.flatnonzero(m))
-            e = make(u[m] - lo, i[m], r[m], hi - lo, n_items, n_factors, kernel, dtype, device,
-                     gamma=gamma, min_rating=min_rating, max_rating=max_rating,
-                     global_mean=global_mean)
-            if waves is None:
-                e.prepare_strata(n_blocks=n_blocks, item_bounds=self.ilo, classes=classes)
-            else:
-                e.prepare_strata(n_blocks=n_blocks, waves=waves, item_bounds=self.ilo,
-                                 classes=classes)
-            self.engines.append(e)
+            self.gidx.append(np.flatnonzero((u >= lo) & (u < hi)))
+        self.sets = [None] * self.K
+        self.ilo = relabel_ranges(i, n_items, world, None)
+        self.engines = self._set(0)
+        self.moves = None
+        self.cur = 0
         # one B for every rank (each rank's plans draw their strata from it)
         self.B = [e.strata.B for e in self.engines]
 
+    def _set(self, q: int) -> list:
+        """The engines of relabelling q (built once, when first needed)."""
+        if self.sets[q] is not None:
+            return self.sets[q]
+        u, i, r, k, kernel, dtype, device, hyp = self._data
+        p = self.perms[q]
+        ilo = relabel_ranges(i, self.n_items, self.world, p)
+        engs = []
+        for rank in range(self.world):
+            lo, hi = int(self.bounds[rank]), int(self.bounds[rank + 1])
+            m = self.gidx[rank]
+            ii = i[m] if p is None else p[i[m]].astype(np.int32)
+            e = self._make(u[m] - lo, ii, r[m], hi - lo, self.n_items, k, kernel, dtype, device,
+                           **hyp)
+            e.prepare_strata(item_bounds=ilo, **self._prep)
+            engs.append(e)
+        if q > 0:                       # P / b_u and the item replica of set 0's shapes
+            base = self.sets[0]
+            Q = torch.empty_like(base[0].Q) if base[0].Q is not None else None
+            bi = torch.empty_like(base[0].bi) if base[0].bi is not None else None
+            for e, b in zip(engs, base):
+                e.P, e.bu = b.P, b.bu
+                e.Q, e.bi = Q, bi
+        self.sets[q] = engs
+        return engs
+
     def load(self, P0, Q0, bu0, bi0) -> None:
-        e0 = self.engines[0]
+        e0 = self.sets[0][0]
         e0.load_params(Q=Q0, bi=bi0)
-        for rank, e in enumerate(self.engines):
+        for rank, e in enumerate(self.sets[0]):
             lo, hi = int(self.bounds[rank]), int(self.bounds[rank + 1])
             e.load_params(P=P0[lo:hi], bu=bu0[lo:hi])
             e.Q, e.bi = e0.Q, e0.bi
+        for q in range(1, self.K):      # relabelled sets built before: re-point P / b_u
+            if self.sets[q] is not None:
+                for e, b in zip(self.sets[q], self.sets[0]):
+                    e.P, e.bu = b.P, b.bu
+        self.cur = 0
+
+    def _to(self, q: int) -> None:
+        if q == self.cur:
+            return
+        engs = self._set(q)
+        src = self.sets[self.cur][0]
+        if engs[0].Q is None:            # built before load(): its replica now
+            Q, bi = torch.empty_like(src.Q), torch.empty_like(src.bi)
+            for e in engs:
+                e.Q, e.bi = Q, bi
+        if self.moves is None:
+            self.moves = _moves(self.perms, getattr(self.sets[0][0], "dev",
+                                                    torch.device("cpu")))
+        relabel_rows(src.Q, engs[0].Q, self.moves, self.cur, q)
+        relabel_rows(src.bi, engs[0].bi, self.moves, self.cur, q)
+        self.cur = q
 
     def epoch(self, draw: int, lr: float, reg: float, update_user=True, update_item=True,
               timing: bool = False, persistent: Optional[bool] = None, epoch: int = 0):
         """Rotation epoch ``epoch`` (its draw ``draw``); with ``timing`` the
         kernel ms of every (sub-epoch, rank) as a world x world array."""
         W = self.world
+        self._to(relabel_pick(draw, self.K))
+        engs = self.sets[self.cur]
         off = rotation_offset(epoch, W)
         ms = np.zeros((W, W))
         for s in range(W):
-            for rank, e in enumerate(self.engines):
+            for rank, e in enumerate(engs):
                 c = rotation_range(rank, off, s, W)
                 seq, seed = rotation_draws(draw, rank, c, e.strata)
                 t = e.epoch_phase(c, seq, seed, lr, reg, update_user, update_item,
@@ -505,10 +780,11 @@ class RotationReplay:
     def serial_order(self, draw: int, epoch: int = 0) -> np.ndarray:
         """Global rating indices in the order epoch ``epoch`` applies them."""
         W = self.world
+        engs = self._set(relabel_pick(draw, self.K))
         off = rotation_offset(epoch, W)
         parts = []
         for s in range(W):
-            for rank, e in enumerate(self.engines):
+            for rank, e in enumerate(engs):
                 c = rotation_range(rank, off, s, W)
                 seq, seed = rotation_draws(draw, rank, c, e.strata)
                 parts.append(self.gidx[rank][e.strata.phase_order(c, seq, seed)])
@@ -516,16 +792,19 @@ class RotationReplay:
 
     def sse(self, slot: int) -> float:
         tot = 0.0
-        for e in self.engines:
+        for e in self.sets[self.cur]:
             e.sse_async(slot)
             tot += float(e.sse_values(slot + 1)[slot])
         return tot
 
     def params(self):
-        """(P, Q, b_u, b_i) float64 host arrays, users in global order."""
-        P = np.concatenate([e.P.cpu().numpy().astype(np.float64) for e in self.engines])
-        bu = np.concatenate([e.bu.cpu().numpy().astype(np.float64) for e in self.engines])
-        e0 = self.engines[0]
+        """(P, Q, b_u, b_i) float64 host arrays, users in global order, items
+        in canonical ids."""
+        self._to(0)
+        engs = self.sets[0]
+        P = np.concatenate([e.P.cpu().numpy().astype(np.float64) for e in engs])
+        bu = np.concatenate([e.bu.cpu().numpy().astype(np.float64) for e in engs])
+        e0 = engs[0]
         return (P, e0.Q.cpu().numpy().astype(np.float64), bu,
                 e0.bi.cpu().numpy().astype(np.float64))
 
@@ -614,7 +893,11 @@ def any_rank_failed(engine: SGDEngine, group=None) -> bool:
     rank since its error word was last cleared (synchronises; one MAX
     all-reduce, so all ranks take the same branch and none is left waiting in
     a collective)."""
-    bad = 1 if (engine.strata is not None and engine.strata_failed()) else 0
+    if isinstance(engine, RotationSet):
+        bad = 1 if engine.failed() else 0
+        engine = engine.main
+    else:
+        bad = 1 if (engine.strata is not None and engine.strata_failed()) else 0
     if not (dist.is_available() and dist.is_initialized()):
         return bool(bad)
     dev = (torch.device("cpu") if dist.get_backend(group) == "gloo"
@@ -629,7 +912,8 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
                 n_epochs: int, kernel: str, n_factors: int, dtype: str, device, gamma: float,
                 min_rating: float, max_rating: float, global_mean: float, lr: float,
                 reg: float, schedule: str, verbose: int = 0, update_user: bool = True,
-                update_item: bool = True, group=None, exchange: str = "rotate"):
+                update_item: bool = True, group=None, exchange: str = "rotate",
+                relabel: int = ROTATE_RELABEL):
     """KernelMF.fit's epochs in process-group mode (every rank calls it with
     the same ratings, initial parameters and NumPy RNG state).
 
@@ -667,11 +951,10 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
     ex = rot = None
     if rotate:
         eng.load_params(Q=Q0, bi=bi0)
-        ilo = item_ranges(i, n_items, world)
-        eng.prepare_strata(item_bounds=ilo)
-        # the RMSE pass of epoch e beside epoch e+1's sub-epochs (side stream)
-        rot = RotationExchange(eng, ilo, group, overlap=True)
-        nb = eng.strata
+        # K item relabellings, one drawn per epoch (RotationSet); the RMSE
+        # pass of epoch e beside epoch e+1's sub-epochs (side stream)
+        rot = RotationSet(eng, i, world, relabel, group, overlap=True)
+        rot.bind()
     else:
         ex = ReplicaExchange(eng, group)
         ex.bind(Q0, bi0)
@@ -686,6 +969,8 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
             nb = len(eng.colored) - 1
     n_total = len(u)
     eng._ensure_sse_slots(n_epochs)       # no reallocation under a side-stream pass
+    if rot is not None:
+        rot.ensure_sse_slots(n_epochs)
     rmse = []
     draws = []
     persistent = None
@@ -695,11 +980,12 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
 
     def run_epoch(epoch, draw, persistent_):
         if rotate:
-            rotation_epoch(eng, rot, draw, lr, reg, update_user, update_item,
-                           persistent=persistent_, epoch=epoch,
-                           sse_slot=epoch if rot.overlap else None)
+            rot.epoch(draw, lr, reg, update_user, update_item, persistent=persistent_,
+                      epoch=epoch, sse_slot=epoch if rot.overlap else None)
             if rot.overlap:
                 return                        # its SSE runs on the side stream
+            rot.engines[rot.cur].sse_async(epoch)     # (its labelling's ratings)
+            return
         else:
             seq, sd = epoch_draws(np.random.RandomState([draw, rank]), nb, strata)
             if strata:
@@ -723,12 +1009,17 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
         eng.restore_params(snap0[0])
         if ex is not None:
             ex.flat.copy_(snap0[1])
-        eng.clear_strata_error()
+        if rot is not None:
+            rot.clear_strata_error()
+            rot.reset()                       # the canonical replica is whole again
+        else:
+            eng.clear_strata_error()
         for ep in range(upto):
             run_epoch(ep, draws[ep], False)
 
     def check(upto):
-        if snap0 is not None and persistent is None and any_rank_failed(eng, group):
+        if snap0 is not None and persistent is None and any_rank_failed(
+                eng if rot is None else rot, group):
             replay(upto)
 
     for epoch in range(n_epochs):
@@ -745,8 +1036,7 @@ def fit_sharded(u: np.ndarray, i: np.ndarray, r: np.ndarray, n_users: int, n_ite
                 print("Epoch ", epoch + 1, "/", n_epochs, " -  train_rmse:", rm)
     check(n_epochs)
     if rot is not None:                   # the whole replica on every rank, all SSEs in
-        rot.gather(rotation_final_ranges(n_epochs - 1, world))
-        rot.join()
+        rot.finish(n_epochs - 1)
     if verbose != 1:
         rmse = global_rmse(eng, n_epochs, n_total, group)
     elif persistent is False:           # a replay re-computed the printed epochs

@@ -52,7 +52,9 @@ Three keyword arguments are new and default to the reference's behaviour:
               cut into one range per rank and the ranges are passed round the
               ring between sub-epochs, so every rating is applied with the
               current user and item rows: a sequential order like the
-              single-GPU schedules) or "delta" (item-row deltas all-reduced
+              single-GPU schedules; which items share a range is redrawn
+              each epoch from 8 fixed item relabellings,
+              distributed.RotationSet) or "delta" (item-row deltas all-reduced
               once per epoch and applied damped: faster per epoch, item
               updates one epoch late).  DESIGN.md section 6 has both measured.
 """

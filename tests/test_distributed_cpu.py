@@ -483,3 +483,69 @@ def test_kernelmf_distributed_rotate_two_ranks(tmp_path):
     P, Q, bu, bi, rmse, _, _ = _replay(world)
     for key, ref in (("P", P), ("Q", Q), ("bu", bu), ("bi", bi), ("rmse", rmse)):
         assert np.max(np.abs(res[0][key] - ref)) < 1e-12, key
+
+
+def test_relabelled_item_ranges_helpers():
+    """The rotation's item relabellings (distributed.RotationSet): fixed
+    permutations drawn from their own RandomStates (the global one is not
+    touched), a pick per epoch draw, balanced ranges over the new ids, and
+    exact row moves between labellings."""
+    from matrix_factorization.distributed import (_moves, item_relabellings, relabel_pick,
+                                                  relabel_ranges, relabel_rows)
+
+    u, i, r, _, _ = _data()
+    st = np.random.get_state()
+    perms = item_relabellings(NI, 8)
+    assert np.array_equal(np.random.get_state()[1], st[1])        # global RNG untouched
+    assert perms[0] is None and len(perms) == 8
+    for p in perms[1:]:
+        assert np.array_equal(np.sort(p), np.arange(NI))
+    assert not np.array_equal(perms[1], perms[2])
+    picks = [relabel_pick(d, 8) for d in range(2000)]
+    assert set(picks) == set(range(8)) and relabel_pick(123, 1) == 0
+    assert picks == [relabel_pick(d, 8) for d in range(2000)]      # a function of the draw
+    for p in perms:
+        b = relabel_ranges(i, NI, 4, p)
+        ids = i if p is None else p[i]
+        cnt = np.array([np.sum((ids >= b[c]) & (ids < b[c + 1])) for c in range(4)])
+        assert b[0] == 0 and b[-1] == NI and cnt.max() - cnt.min() <= 2 * np.bincount(i).max()
+    mv = _moves(perms, torch.device("cpu"))
+    Q = torch.as_tensor(np.random.RandomState(3).normal(size=(NI, K)))
+    A, Bq, C = torch.empty_like(Q), torch.empty_like(Q), torch.empty_like(Q)
+    relabel_rows(Q, A, mv, 0, 3)                  # canonical -> labelling 3
+    assert torch.equal(A[torch.as_tensor(perms[3])], Q)
+    relabel_rows(A, Bq, mv, 3, 5)                 # 3 -> 5
+    assert torch.equal(Bq[torch.as_tensor(perms[5])], Q)
+    relabel_rows(Bq, C, mv, 5, 0)                 # 5 -> canonical
+    assert torch.equal(C, Q)
+
+
+@pytest.mark.timeout(300)
+def test_rotation_relabel_one_is_the_plain_rotation():
+    """relabel=1 is the rotation without relabellings (the round-5 product
+    path), and the default (8 relabellings) trains a different sequential
+    order from the same draws -- the relabellings are in use."""
+    from matrix_factorization.distributed import RotationReplay, relabel_pick
+
+    u, i, r, nu, ni, P0, Q0, mu = _mapped()
+    draws = [int(d) for d in np.random.RandomState(4).randint(0, 2**31 - 1, EPOCHS)]
+    assert any(relabel_pick(d, 8) != 0 for d in draws)
+    out = {}
+    for K_ in (1, 8):
+        rp = RotationReplay(u, i, r, nu, ni, 2, K, "linear", "float64", None,
+                            global_mean=mu, engine_cls=_cpu_engine_factory, relabel=K_)
+        rp.load(P0, Q0, np.zeros(nu), np.zeros(ni))
+        orders = []
+        for ep, d in enumerate(draws):
+            orders.append(rp.serial_order(d, ep))
+            rp.epoch(d, LR, REG, epoch=ep)
+        out[K_] = (orders, rp.params())
+    # K = 1: the plain rotation's order, item ranges over canonical ids
+    from matrix_factorization.distributed import item_ranges
+    ilo = item_ranges(i, ni, 2)
+    first = out[1][0][0]                     # epoch 0 starts with rank 0's first range
+    c0 = (i[first[:10]] >= ilo[0]) & (i[first[:10]] < ilo[1])
+    assert c0.all() or (~c0).all()
+    # relabelled epochs are another order (and another model)
+    assert any(not np.array_equal(a, b) for a, b in zip(out[1][0], out[8][0]))
+    assert np.max(np.abs(out[1][1][1] - out[8][1][1])) > 0
