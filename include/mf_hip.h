@@ -297,9 +297,11 @@ int32_t mf_strata_slots_waves(int32_t n_factors, int32_t dtype, int32_t waves);
  * double *sse_out (no host sync).  `workspace` is a device buffer of at
  * least mf_sse_workspace_bytes(n_ratings) bytes.  Deterministic: the same
  * inputs give the same bits.
- * slice_offsets (HOST, nullable, n_slices + 1 <= 17 entries): the ratings
+ * slice_offsets (HOST, nullable, n_slices + 1 <= 129 entries): the ratings
  * are ordered by mf_sched_slices; slice x is walked by the workgroups
- * b % n_slices == x (XCD-local Q slices).  NULL = one slice.
+ * b % n_slices == x (XCD-local Q slices).  NULL = one slice.  n_slices > 8
+ * and a multiple of 8 (mf_sched_tiles): the tiles are walked in phases of 8,
+ * by a resident grid for FP64 (MF_SSE_PHASED=0: dispatch-ordered phases).
  * n_users / n_items: rows of user_features / item_features (every id must
  * be below them).
  */
@@ -572,6 +574,25 @@ int mf_sched_slices(const int32_t* user_ids, const int32_t* item_ids,
                     int64_t n, int32_t n_users, int32_t n_items,
                     int32_t n_slices, int32_t* sched_out,
                     int64_t* slice_offsets);
+
+/*
+ * Tiled evaluation order (replaces the per-rating loop order of
+ * _calculate_rmse, kernel_matrix_factorization.py:240-317, which any order
+ * serves: the pass is read-only).  Users are cut into n_chunks contiguous id
+ * ranges of about equal rating counts, items into n_slices id ranges; tile
+ * c * n_slices + s holds the ratings of user chunk c and item slice s, users
+ * ascending inside a tile.  With n_slices a multiple of 8 and the offsets
+ * passed to mf_sse, the FP64 pass walks the tiles in phases of 8 (one per
+ * XCD) with a resident grid (k_sse_phased), so each XCD's L2 holds one
+ * 1/n_slices item slice at a time.
+ *   n_chunks * n_slices <= 128
+ *   sched_out      host, n: rating indices in that order
+ *   tile_offsets   host, n_chunks * n_slices + 1
+ */
+int mf_sched_tiles(const int32_t* user_ids, const int32_t* item_ids,
+                   int64_t n, int32_t n_users, int32_t n_items,
+                   int32_t n_chunks, int32_t n_slices, int32_t* sched_out,
+                   int64_t* tile_offsets);
 
 /*
  * Plan of the stratified sweep (mf_sgd_epoch_strata), host only.

@@ -125,7 +125,7 @@ constexpr uint32_t kBufDropRd = 0xFFFFFFF0u;
 // Work split of the read-only passes: `n` slices of the rating array (the
 // item-range slices of mf_sched_slices), slice x walked by the workgroups
 // b with b % n == x.  Placement only changes speed.
-constexpr int kMaxSlices = 16;
+constexpr int kMaxSlices = 128;
 struct SliceTab {
     int64_t off[kMaxSlices + 1];
     int32_t n;
@@ -746,8 +746,10 @@ __global__ __launch_bounds__(kBlock) void k_sse_owned(ReadArgs<T> A, SliceTab SL
 //  * live ratings counted in int32 per step; the FP64 square-add of FP32
 //    errors as one v_fma_f64 (err^2 is exact in FP64, so fma == mul + add)
 //    of an error zeroed on idle slots and on non-lead lanes.
+// The walk of k_sse_lean over one wave's share [b0, b1) of the evaluation
+// order; returns the lane's part of the FP64 SSE (non-lead lanes: 0).
 template <typename T, int W, int GS, int V, int KERN, int S, bool U24>
-__global__ __launch_bounds__(kBlock) void k_sse_lean(ReadArgs<T> A, SliceTab SL) {
+__device__ __forceinline__ double sse_lean_range(const ReadArgs<T>& A, int64_t b0, int64_t b1) {
     using VT = typename VecOf<T, W>::type;
     constexpr int R = kWave / GS;
     static_assert(GS % S == 0, "a chunk of GS ratings is whole steps");
@@ -757,10 +759,6 @@ __global__ __launch_bounds__(kBlock) void k_sse_lean(ReadArgs<T> A, SliceTab SL)
     const int k = A.k;
     const int kv = k / W;
     const Hyper<T> h = A.h;
-    const SliceWave sw = slice_wave(SL);
-    const int64_t s0 = SL.off[sw.x], len = SL.off[sw.x + 1] - s0;
-    const int64_t b0 = s0 + len * sw.wv / sw.nw;
-    const int64_t b1 = s0 + len * (sw.wv + 1) / sw.nw;
     double acc = 0.0;
     if (b0 < b1) {
         const int64_t wl = b1 - b0;
@@ -874,17 +872,58 @@ __global__ __launch_bounds__(kBlock) void k_sse_lean(ReadArgs<T> A, SliceTab SL)
         if (kv == GS * V) sweep(std::true_type{});
         else sweep(std::false_type{});
     }
+    return acc;
+}
+
+__device__ __forceinline__ void sse_block_partial(double acc, double* partials) {
     acc = wave_sum(acc);
     __shared__ double red[kWavesPerBlock];
-    if (lane == 0) red[threadIdx.x / kWave] = acc;
+    if ((threadIdx.x & (kWave - 1)) == 0) red[threadIdx.x / kWave] = acc;
     __syncthreads();
     if (threadIdx.x == 0) {
         double t = 0.0;
 #pragma unroll
         for (int w = 0; w < kWavesPerBlock; ++w) t += red[w];
-        A.partials[blockIdx.x] = t;
+        partials[blockIdx.x] = t;
     }
 }
+
+template <typename T, int W, int GS, int V, int KERN, int S, bool U24>
+__global__ __launch_bounds__(kBlock) void k_sse_lean(ReadArgs<T> A, SliceTab SL) {
+    const SliceWave sw = slice_wave(SL);
+    const int64_t s0 = SL.off[sw.x], len = SL.off[sw.x + 1] - s0;
+    const int64_t b0 = s0 + len * sw.wv / sw.nw;
+    const int64_t b1 = s0 + len * (sw.wv + 1) / sw.nw;
+    sse_block_partial(sse_lean_range<T, W, GS, V, KERN, S, U24>(A, b0, b1), A.partials);
+}
+
+// Training SSE over TILES walked in phases by a resident grid (the FP64
+// pass; DESIGN.md section 5, "FP64 RMSE pass").  The evaluation order is
+// cut into n = 8 P tiles (mf_sched_tiles: user chunk c x item slice s,
+// tile c * S + s, users ascending inside a tile); phase ph = tile / 8 and
+// block b walks, phase after phase, its share of tile 8 ph + (b mod 8).
+// With one block per resident slot every block of an XCD (b mod 8 under
+// the observed round-robin placement -- speed only) is in about the same
+// phase at the same time, so the XCD's L2 serves one item slice (and one
+// user chunk's rows) instead of the several a dispatch-ordered grid has in
+// flight.  Same ratings per wave-share, same per-rating arithmetic and the
+// same FP64 sum per lane as k_sse_lean.
+template <typename T, int W, int GS, int V, int KERN, int S, bool U24>
+__global__ __launch_bounds__(kBlock) void k_sse_phased(ReadArgs<T> A, SliceTab SL) {
+    const int64_t per_x = gridDim.x / 8;                        // blocks per XCD
+    const int64_t nw = per_x * kWavesPerBlock;
+    const int64_t wv = (int64_t)(blockIdx.x / 8) * kWavesPerBlock + threadIdx.x / kWave;
+    const int xb = (int)(blockIdx.x % 8);
+    double acc = 0.0;
+    for (int ph = 0; ph < SL.n / 8; ++ph) {
+        const int x = 8 * ph + xb;
+        const int64_t s0 = SL.off[x], len = SL.off[x + 1] - s0;
+        acc += sse_lean_range<T, W, GS, V, KERN, S, U24>(A, s0 + len * wv / nw,
+                                                          s0 + len * (wv + 1) / nw);
+    }
+    sse_block_partial(acc, A.partials);
+}
+
 
 // Training SSE, software-pipelined form of k_sse_owned (same ratings, same
 // owned user rows, same per-rating arithmetic).  A group's run is cut into
@@ -1266,8 +1305,21 @@ struct SseRun {
             if (var == 0 && ev && std::atoi(ev) == 4) { var = 4; kfn = k_sse_pipe<T, W, GS, V, KERN, 8>; }
             if (var == 0 && ev && std::atoi(ev) == 5) { var = 5; kfn = k_sse_pipe<T, W, GS, V, KERN, 4>; }
         }
+        // tiles walked in phases by a resident grid (mf_sched_tiles order:
+        // n > 8, a multiple of 8); MF_SSE_PHASED=0 walks them as a
+        // dispatch-ordered grid (slice_wave) instead
+        const char* ep = std::getenv("MF_SSE_PHASED");
+        const bool phased = var == 0 && p.S.n > 8 && p.S.n % 8 == 0 && !(ep && ep[0] == '0');
+        if (phased) {
+            var = u24 ? 10 : 11;
+            kfn = u24 ? k_sse_phased<T, W, GS, V, KERN, S, true>
+                      : k_sse_phased<T, W, GS, V, KERN, S, false>;
+            if constexpr (GS == 16 && V == 1 && std::is_same<T, float>::value)
+                kfn = u24 ? k_sse_phased<T, W, GS, V, KERN, 16, true>
+                          : k_sse_phased<T, W, GS, V, KERN, 16, false>;
+        }
         if (var == 0 && !u24) var = 7;                    // its own occupancy entry
-        static int resident_tab[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // per instantiation and variant
+        static int resident_tab[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // per instantiation and variant
         int& resident = resident_tab[var];
         if (resident == 0) {
             const LaunchTrace lt;
@@ -1287,12 +1339,19 @@ struct SseRun {
         int blocks = (int)std::min<int64_t>(
             std::max<int64_t>(resident, std::min<int64_t>(by_size, 8 * (int64_t)resident)),
             kSseMaxBlocks);
+        // phased: one block per resident slot (all of an XCD's blocks move
+        // through the phases together)
+        if (phased) blocks = std::min(resident, kSseMaxBlocks);
         if (const char* e = std::getenv("MF_SSE_BLOCKS")) {
             const int v = std::atoi(e);
             if (v > 0) blocks = std::min(v, kSseMaxBlocks);
         }
         if (p.max_blocks > 0) blocks = std::min(blocks, p.max_blocks);
-        blocks = std::max(p.S.n, (blocks / p.S.n) * p.S.n);
+        if (phased) {
+            blocks = std::max(8, (blocks / 8) * 8);      // a multiple of 8
+        } else {
+            blocks = std::max(p.S.n, (blocks / p.S.n) * p.S.n);
+        }
         const LaunchTrace lt2;
         hipLaunchKernelGGL(kfn, dim3(blocks), dim3(kBlock), 0, p.stream, a, p.S);
         hipLaunchKernelGGL(k_sum_partials, dim3(1), dim3(kBlock), 0, p.stream,

@@ -349,6 +349,29 @@ extern "C" int mf_sched_color(const int32_t* user_ids, const int32_t* item_ids, 
     return MF_OK;
 }
 
+// Rows bucketed by key (a stable partition), then users ascending inside
+// each bucket (a stable counting sort): the evaluation orders of the SSE pass.
+template <typename Key>
+static void sched_by_key_then_user(const int32_t* user_ids, int64_t n, int32_t n_users,
+                                   int32_t n_keys, Key key, int32_t* sched_out,
+                                   int64_t* offsets) {
+    const int T = mf::host_threads();
+    std::vector<int64_t> start;
+    mf::partition_rows(
+        n, n_keys, T, key, start, [&](int64_t d, int64_t p) { sched_out[d] = (int32_t)p; });
+    for (int32_t x = 0; x <= n_keys; ++x) offsets[x] = start[x];
+    mf::for_buckets(n_keys, T, [&](int s) {
+        int32_t* q = sched_out + start[s];
+        const int64_t m = start[s + 1] - start[s];
+        std::vector<int64_t> cnt((size_t)n_users + 1, 0);
+        for (int64_t j = 0; j < m; ++j) cnt[user_ids[q[j]] + 1] += 1;
+        for (int32_t x = 0; x < n_users; ++x) cnt[x + 1] += cnt[x];
+        std::vector<int32_t> tmp((size_t)m);
+        for (int64_t j = 0; j < m; ++j) tmp[cnt[user_ids[q[j]]]++] = q[j];
+        std::copy(tmp.begin(), tmp.end(), q);
+    });
+}
+
 extern "C" int mf_sched_slices(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
                                int32_t n_users, int32_t n_items, int32_t n_slices,
                                int32_t* sched_out, int64_t* slice_offsets) {
@@ -364,24 +387,46 @@ extern "C" int mf_sched_slices(const int32_t* user_ids, const int32_t* item_ids,
         auto slice_of = [&](int32_t it) {
             return (int)((int64_t)it * n_slices / (n_items > 0 ? n_items : 1));
         };
-        const int T = mf::host_threads();
-        std::vector<int64_t> start;
-        mf::partition_rows(
-            n, n_slices, T, [&](int64_t p) { return slice_of(item_ids[p]); }, start,
-            [&](int64_t d, int64_t p) { sched_out[d] = (int32_t)p; });
-        for (int32_t x = 0; x <= n_slices; ++x) slice_offsets[x] = start[x];
-        mf::for_buckets(n_slices, T, [&](int s) {
-            int32_t* q = sched_out + start[s];
-            const int64_t m = start[s + 1] - start[s];
-            std::vector<int64_t> cnt((size_t)n_users + 1, 0);
-            for (int64_t j = 0; j < m; ++j) cnt[user_ids[q[j]] + 1] += 1;
-            for (int32_t x = 0; x < n_users; ++x) cnt[x + 1] += cnt[x];
-            std::vector<int32_t> tmp((size_t)m);
-            for (int64_t j = 0; j < m; ++j) tmp[cnt[user_ids[q[j]]]++] = q[j];
-            std::copy(tmp.begin(), tmp.end(), q);
-        });
+        sched_by_key_then_user(user_ids, n, n_users, n_slices,
+                               [&](int64_t p) { return slice_of(item_ids[p]); }, sched_out,
+                               slice_offsets);
     } catch (const std::bad_alloc&) {
         set_error("mf_sched_slices: out of host memory");
+        return MF_ERR_NOMEM;
+    }
+    return MF_OK;
+}
+
+extern "C" int mf_sched_tiles(const int32_t* user_ids, const int32_t* item_ids, int64_t n,
+                              int32_t n_users, int32_t n_items, int32_t n_chunks,
+                              int32_t n_slices, int32_t* sched_out, int64_t* tile_offsets) {
+    if (n < 0 || n_users < 0 || n_items < 0 || n_chunks < 1 || n_slices < 1 ||
+        (int64_t)n_chunks * n_slices > 128 || (n > 0 && !sched_out) || !tile_offsets) {
+        set_error("mf_sched_tiles: bad arguments (n_chunks * n_slices must be in [1, 128])");
+        return MF_ERR_INVALID;
+    }
+    if (int rc = check_ids(user_ids, item_ids, n, n_users, n_items)) return rc;
+    try {
+        // user chunks: contiguous id ranges of about equal rating counts
+        std::vector<int64_t> deg((size_t)n_users + 1, 0);
+        for (int64_t p = 0; p < n; ++p) deg[(size_t)user_ids[p] + 1] += 1;
+        for (int32_t x = 0; x < n_users; ++x) deg[x + 1] += deg[x];
+        std::vector<uint8_t> chunk_of((size_t)n_users, 0);
+        int32_t c = 0;
+        for (int32_t x = 0; x < n_users; ++x) {
+            // user x goes to the chunk its first rating's rank falls in
+            while (c + 1 < n_chunks && deg[x] * n_chunks >= (int64_t)(c + 1) * n) ++c;
+            chunk_of[x] = (uint8_t)c;
+        }
+        auto slice_of = [&](int32_t it) {
+            return (int)((int64_t)it * n_slices / (n_items > 0 ? n_items : 1));
+        };
+        sched_by_key_then_user(
+            user_ids, n, n_users, n_chunks * n_slices,
+            [&](int64_t p) { return (int)chunk_of[user_ids[p]] * n_slices + slice_of(item_ids[p]); },
+            sched_out, tile_offsets);
+    } catch (const std::bad_alloc&) {
+        set_error("mf_sched_tiles: out of host memory");
         return MF_ERR_NOMEM;
     }
     return MF_OK;

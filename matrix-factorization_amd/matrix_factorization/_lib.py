@@ -117,6 +117,7 @@ SIGNATURES = {
     "mf_sched_color": (ctypes.c_int, [
         _P, _P, _I64, _I32, _I32, _P, _P, _I64, _P]),
     "mf_sched_slices": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _I32, _P, _P]),
+    "mf_sched_tiles": (ctypes.c_int, [_P, _P, _I64, _I32, _I32, _I32, _I32, _P, _P]),
     "mf_strata_plan_build": (ctypes.c_int, [
         _P, _P, _I64, _I32, _I32, _I32, _P, _P, _I32, _P]),
     "mf_strata_plan_build_classes": (ctypes.c_int, [

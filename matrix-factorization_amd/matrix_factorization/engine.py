@@ -177,6 +177,33 @@ def sched_slices(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int,
 N_SLICES = 8          # one item slice per XCD (MI355X: 8 XCDs x 4 MiB L2)
 
 
+def sched_tiles(u: np.ndarray, i: np.ndarray, n_users: int, n_items: int, n_chunks: int,
+                n_slices: int) -> Tuple[np.ndarray, np.ndarray]:
+    """Evaluation order in tiles (mf_sched_tiles): user chunk x item slice,
+    users ascending inside a tile; (1, S) is sched_slices(S)."""
+    n = len(u)
+    u = np.ascontiguousarray(u, np.int32)
+    i = np.ascontiguousarray(i, np.int32)
+    sched = np.empty(n, np.int32)
+    offs = np.empty(n_chunks * n_slices + 1, np.int64)
+    _lib.call("mf_sched_tiles", _np(u), _np(i), n, n_users, n_items, n_chunks, n_slices,
+              _np(sched), _np(offs))
+    return sched, offs
+
+
+# the training-RMSE pass's evaluation tiles (user chunks, item slices) per
+# dtype; env MF_SSE_TILES="C,S" overrides (probes: tools/sse_tiles_probe.py)
+EVAL_TILES = {"float32": (1, N_SLICES), "float64": (1, N_SLICES)}
+
+
+def eval_tiles(dtype: str) -> Tuple[int, int]:
+    env = os.environ.get("MF_SSE_TILES")
+    if env:
+        c, s_ = (int(x) for x in env.split(","))
+        return c, s_
+    return EVAL_TILES.get(dtype, (1, N_SLICES))
+
+
 # ------------------------------------------------------------ strata plan
 def strata_mix(seed: int, blk: int) -> int:
     """First colour of block ``blk`` (mod its colour count) in the epoch with
@@ -682,8 +709,9 @@ class SGDEngine:
         if self.bias_only or self.n == 0:
             self.eu, self.ei, self.er, self.eval_offs = self.u, self.i, self.r, None
             return
-        sched, offs = sched_slices(self.u_host, self.i_host, self.n_users, self.n_items,
-                                   N_SLICES)
+        n_chunks, n_slices = eval_tiles(self.dtype)
+        sched, offs = sched_tiles(self.u_host, self.i_host, self.n_users, self.n_items,
+                                  n_chunks, n_slices)
         # reorder on the device from the uploaded triples (one int32 upload
         # instead of three host gathers of n elements)
         d_sched = torch.from_numpy(sched).to(self.dev).long()

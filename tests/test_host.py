@@ -395,6 +395,42 @@ def test_slice_order_groups_items_then_users():
 
 
 # ------------------------------------------------------------ strata plan
+def test_tile_order_chunks_users_and_slices_items():
+    """mf_sched_tiles (the FP64 RMSE pass's evaluation order): (1, S) is
+    mf_sched_slices(S) exactly; tile c * S + s holds the ratings of user
+    chunk c (contiguous id ranges of about equal rating counts) and item
+    slice s, users ascending (stable) inside a tile."""
+    from matrix_factorization.engine import sched_slices, sched_tiles
+
+    rs = np.random.RandomState(5)
+    nu, ni, n = 3000, 700, 60000
+    u = rs.randint(0, nu, n).astype(np.int32)
+    i = rs.randint(0, ni, n).astype(np.int32)
+    a, oa = sched_slices(u, i, nu, ni, 8)
+    b, ob = sched_tiles(u, i, nu, ni, 1, 8)
+    assert np.array_equal(a, b) and np.array_equal(oa, ob)
+    C, S = 4, 16
+    t, ot = sched_tiles(u, i, nu, ni, C, S)
+    assert np.array_equal(np.sort(t), np.arange(n)) and ot[0] == 0 and ot[-1] == n
+    chunk_hi = []
+    for c in range(C):
+        for s_ in range(S):
+            rows = t[ot[c * S + s_]:ot[c * S + s_ + 1]]
+            assert np.all(i[rows] * S // ni == s_)
+            assert np.all(np.diff(u[rows]) >= 0)
+            eq = np.diff(u[rows]) == 0                     # stable inside a user
+            assert np.all(np.diff(rows)[eq] > 0)
+        rows = t[ot[c * S]:ot[(c + 1) * S]]
+        chunk_hi.append((u[rows].min(), u[rows].max(), len(rows)))
+    for c in range(C - 1):
+        assert chunk_hi[c][1] < chunk_hi[c + 1][0]         # contiguous user ranges
+    sizes = np.array([x[2] for x in chunk_hi])
+    assert sizes.max() - sizes.min() < 0.02 * n
+    from matrix_factorization import _lib
+    with pytest.raises(_lib.MFLibraryError):
+        sched_tiles(u, i, nu, ni, 16, 16)                  # > 128 tiles
+
+
 @pytest.mark.parametrize("B,NS,C", [(1, 32, 1), (3, 16, 1), (8, 128, 1), (1, 32, 2),
                                     (3, 16, 2), (8, 64, 3), (5, 32, 4)])
 def test_strata_plan_is_valid(B, NS, C):
