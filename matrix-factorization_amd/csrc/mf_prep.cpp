@@ -163,6 +163,81 @@ void shuffle_raw(MT& mt, E* data, int64_t n) {
     }
 }
 
+// The same shuffle on two threads: this one draws (MT twist, temper, the
+// branch-free rejection of shuffle_raw) into a ring of swap targets, a second
+// one applies the swaps in order, prefetching each target kAhead swaps ahead
+// in its own cache.  Same outputs consumed, same targets, the same swaps in
+// the same order: the result and the MT state afterwards are shuffle_raw's.
+// The two stages hand over chunks of kChunk targets through two counters.
+template <typename E>
+void shuffle_raw_2t(MT& mt, E* data, int64_t n) {
+    if (n < 2) return;
+    const int64_t total = n - 1;
+    constexpr int64_t kR = 1 << 16, kChunk = 1 << 11, kAhead = 48;
+    std::unique_ptr<uint32_t[]> ring(new uint32_t[kR]);
+    alignas(64) std::atomic<int64_t> drawn{0};
+    alignas(64) std::atomic<int64_t> done{0};
+    std::thread swapper([&]() {
+        uint32_t* rg = ring.get();
+        int64_t d = 0, avail = 0;
+        while (d < total) {
+            while (avail <= d) {                       // wait for the next chunk
+                avail = drawn.load(std::memory_order_acquire);
+                if (avail <= d) std::this_thread::yield();
+            }
+            const int64_t lim = avail;
+            for (; d < lim; ++d) {
+                if (d + kAhead < lim) __builtin_prefetch(data + rg[(d + kAhead) & (kR - 1)], 1, 1);
+                const int64_t i = total - d;
+                const int64_t j = rg[d & (kR - 1)];
+                const E t = data[i];
+                data[i] = data[j];
+                data[j] = t;
+                if ((d & (kChunk - 1)) == kChunk - 1) done.store(d + 1, std::memory_order_release);
+            }
+        }
+        done.store(total, std::memory_order_release);
+    });
+    uint32_t* rg = ring.get();
+    int64_t d = 0;
+    uint32_t maxv = (uint32_t)total;
+    int64_t pub = 0;
+    while (d < total) {
+        // room for a whole MT block of targets (<= kN) in the ring
+        while (d + kN - done.load(std::memory_order_acquire) > kR) std::this_thread::yield();
+        if (mt.pos == kN) mt.regen();
+        int p = mt.pos;
+        while (p < kN) {
+            const uint32_t mask = 0xffffffffu >> __builtin_clz(maxv);
+            const uint32_t v = mt_temper(mt.key[p++]) & mask;
+            const uint32_t acc = v <= maxv ? 1u : 0u;
+            rg[d & (kR - 1)] = v;
+            d += acc;
+            maxv -= acc;
+            if (d == total) break;
+        }
+        mt.pos = p;
+        if (d - pub >= kChunk || d == total) {
+            drawn.store(d, std::memory_order_release);
+            pub = d;
+        }
+    }
+    swapper.join();
+}
+
+// shuffle_raw, on two threads from this many elements (MF_SHUFFLE_THREADS=1
+// keeps one)
+constexpr int64_t kShuffle2tMin = 1 << 22;
+
+template <typename E>
+void shuffle_any(MT& mt, E* data, int64_t n) {
+    const char* env = std::getenv("MF_SHUFFLE_THREADS");
+    if (n >= kShuffle2tMin && !(env && env[0] == '1'))
+        shuffle_raw_2t(mt, data, n);
+    else
+        shuffle_raw(mt, data, n);
+}
+
 int load_mt(MT& mt, const uint32_t* mt_key, const int32_t* mt_pos, int64_t n, const char* who) {
     if (n - 1 > (int64_t)0xffffffffLL) {
         set_error("%s: n = %lld exceeds the 32-bit draw range", who, (long long)n);
@@ -186,7 +261,7 @@ extern "C" int mf_legacy_shuffle(uint32_t* mt_key, int32_t* mt_pos, int64_t* dat
     }
     MT mt;
     if (const int rc = load_mt(mt, mt_key, mt_pos, n, "mf_legacy_shuffle")) return rc;
-    shuffle_raw(mt, data, n);
+    shuffle_any(mt, data, n);
     std::memcpy(mt_key, mt.key, sizeof(mt.key));
     *mt_pos = mt.pos;
     return MF_OK;
@@ -201,7 +276,7 @@ extern "C" int mf_legacy_shuffle_i32(uint32_t* mt_key, int32_t* mt_pos, int32_t*
     }
     MT mt;
     if (const int rc = load_mt(mt, mt_key, mt_pos, n, "mf_legacy_shuffle_i32")) return rc;
-    shuffle_raw(mt, data, n);
+    shuffle_any(mt, data, n);
     std::memcpy(mt_key, mt.key, sizeof(mt.key));
     *mt_pos = mt.pos;
     return MF_OK;
@@ -222,7 +297,7 @@ extern "C" int mf_legacy_permutation(uint32_t* mt_key, int32_t* mt_pos, int64_t*
         parallel_chunks(n, T, [&](int, int64_t a, int64_t b) {
             for (int64_t p = a; p < b; ++p) out[p] = p;
         });
-        shuffle_raw(mt, out, n);
+        shuffle_any(mt, out, n);
     } else {
         big_ptr<uint32_t> tmp{nullptr, MapFree{0}};
         try {
@@ -235,7 +310,7 @@ extern "C" int mf_legacy_permutation(uint32_t* mt_key, int32_t* mt_pos, int64_t*
         parallel_chunks(n, T, [&](int, int64_t a, int64_t b) {
             for (int64_t p = a; p < b; ++p) tmp[p] = (uint32_t)p;
         });
-        shuffle_raw(mt, tmp.get(), n);
+        shuffle_any(mt, tmp.get(), n);
         parallel_chunks(n, T, [&](int, int64_t a, int64_t b) {
             for (int64_t p = a; p < b; ++p) out[p] = tmp[p];
         });

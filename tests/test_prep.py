@@ -47,12 +47,19 @@ def test_legacy_shuffle_mid_stream():
         assert np.array_equal(a, b) and np.array_equal(x1, x2), draws
 
 
+@pytest.mark.parametrize("threads", [None, "1"])
 @pytest.mark.parametrize("dtype,n,draws", [(np.int32, 5_000_000, 0), (np.int32, 4_194_305, 623),
                                            (np.int64, 4_500_001, 624), (np.int32, 6_000_011, 5)])
-def test_large_shuffle_is_numpys(dtype, n, draws):
+def test_large_shuffle_is_numpys(dtype, n, draws, threads, monkeypatch):
     """Millions of elements (the prefetch ring wraps many times, the MT state
     crosses thousands of 624-word blocks): the same permutation and the same
-    RandomState afterwards as np.random.shuffle, from any MT position."""
+    RandomState afterwards as np.random.shuffle, from any MT position -- on
+    the two-thread form (draws / swaps, the default from 2^22 elements) and
+    on one thread (MF_SHUFFLE_THREADS=1)."""
+    if threads is None:
+        monkeypatch.delenv("MF_SHUFFLE_THREADS", raising=False)
+    else:
+        monkeypatch.setenv("MF_SHUFFLE_THREADS", threads)
     np.random.seed(19)
     np.random.randint(0, 10, draws)
     st = np.random.get_state()
@@ -62,6 +69,23 @@ def test_large_shuffle_is_numpys(dtype, n, draws):
     np.random.set_state(st)
     b = np.arange(n, dtype=dtype)
     _prep.legacy_shuffle_(b)
+    x2 = np.random.rand(3)
+    assert np.array_equal(a, b) and np.array_equal(x1, x2)
+
+
+@pytest.mark.parametrize("threads", [None, "1"])
+def test_large_permutation_is_numpys(threads, monkeypatch):
+    """np.random.permutation(n) at 5M (fit()'s X.sample(frac=1) draw), both
+    shuffle forms: the same permutation and RandomState afterwards."""
+    if threads is None:
+        monkeypatch.delenv("MF_SHUFFLE_THREADS", raising=False)
+    else:
+        monkeypatch.setenv("MF_SHUFFLE_THREADS", threads)
+    np.random.seed(23)
+    a = np.random.permutation(5_000_003)
+    x1 = np.random.rand(3)
+    np.random.seed(23)
+    b = _prep.legacy_permutation(5_000_003)
     x2 = np.random.rand(3)
     assert np.array_equal(a, b) and np.array_equal(x1, x2)
 

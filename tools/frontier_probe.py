@@ -23,6 +23,10 @@ Designs (--designs, any of):
                       epoch (which items share a range changes epoch to
                       epoch; the ranges are all-gathered anyway);
   rotcls<M>rel<K>     both of the above;
+  rotprod<K>          the PRODUCT path: distributed.RotationReplay with K item
+                      relabellings (relabel_pick of each epoch's draw, the
+                      replica moved between labellings) -- the bench / fit
+                      default since round 6 is rotprod8;
   rotc<C>[b<B>]       the rotation with sub-block plans of C user-range classes
                       (and B blocks): the stream kernel applies from C = 2;
   delta<M>s<S>        user-sharded replicas, the stratum order of each rank's
@@ -220,6 +224,26 @@ def main():
         del sets
         torch.cuda.empty_cache()
 
+    def run_prod(name, relabel):
+        rp = RotationReplay(u, i, r, nu, ni, W, k, kernel, "float32", dev, relabel=relabel, **hyp)
+        sweep = []
+        for s in args.draw_seeds:
+            rp.load(P0, Q0, np.zeros(nu), np.zeros(ni))
+            rm = []
+            for ep in range(E):
+                draw = int(np.random.RandomState([s, ep, W]).randint(0, 2**31 - 1))
+                ms = rp.epoch(draw, lr, reg, timing=True, epoch=ep)
+                sweep.append(float(ms.max(axis=1).sum()))      # per sub-epoch: slowest rank
+                rm.append(float(np.sqrt(rp.sse(ep) / nnz)))
+            runs.append({"family": name, "seed": s, "rmse": rm})
+            log(f"{name} seed {s}: final {rm[-1]:.7f}")
+        rows = ni // W
+        xch = (W - 1) * t_pass(rows) + (W - 1) * t_pass(rows)
+        timing[name] = {"sweep_ms": float(np.median(sweep)), "exchange_ms_model": xch,
+                        "relabel": relabel}
+        del rp
+        torch.cuda.empty_cache()
+
     def run_delta(name, rounds, scale):
         parts = shard_engines(1)
         engs = []
@@ -295,6 +319,8 @@ def main():
             run_rotate(d, sub=int(m), relabel=int(kk))
         elif d.startswith("rotcls"):
             run_rotate(d, sub=int(d[6:]))
+        elif d.startswith("rotprod"):
+            run_prod(d, int(d[7:]))
         elif d.startswith("rotrel"):
             run_rotate(d, relabel=int(d[6:]))
         elif d.startswith("rotc"):                 # rotc<C>[b<B>]: sub-block plans of C classes
