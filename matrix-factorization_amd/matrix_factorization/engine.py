@@ -710,16 +710,47 @@ class SGDEngine:
             self.eu, self.ei, self.er, self.eval_offs = self.u, self.i, self.r, None
             return
         n_chunks, n_slices = eval_tiles(self.dtype)
-        sched, offs = sched_tiles(self.u_host, self.i_host, self.n_users, self.n_items,
-                                  n_chunks, n_slices)
-        # reorder on the device from the uploaded triples (one int32 upload
-        # instead of three host gathers of n elements)
-        d_sched = torch.from_numpy(sched).to(self.dev).long()
+        if os.environ.get("MF_EVAL_ORDER") == "host":
+            sched, offs = sched_tiles(self.u_host, self.i_host, self.n_users, self.n_items,
+                                      n_chunks, n_slices)
+            d_sched = torch.from_numpy(sched).to(self.dev).long()
+        else:
+            d_sched, offs = self._eval_order_device(n_chunks, n_slices)
+        # reorder on the device from the uploaded triples
         self.eu = self.u.index_select(0, d_sched)
         self.ei = self.i.index_select(0, d_sched)
         self.er = self.r.index_select(0, d_sched)
         del d_sched
         self.eval_offs = offs
+
+    def _eval_order_device(self, n_chunks: int, n_slices: int):
+        """mf_sched_tiles' order computed on the GPU from the uploaded ids:
+        a stable sort of key = (user chunk * n_slices + item slice) * n_users
+        + user -- the host order exactly (tiles by a stable partition, users
+        ascending, ties in rating order), in ~tens of ms instead of the
+        host's ~0.4 s at C3 (fit()'s engine build)."""
+        with torch.cuda.device(self.dev):
+            u = self.u.long()
+            i = self.i.long()
+            n, nu = self.n, self.n_users
+            sl = torch.div(i * n_slices, max(self.n_items, 1), rounding_mode="floor")
+            if n_chunks > 1:
+                deg = torch.bincount(u, minlength=nu)
+                before = torch.cumsum(deg, 0) - deg            # ratings of users < x
+                chunk_of = torch.clamp(torch.div(before * n_chunks, n, rounding_mode="floor"),
+                                       max=n_chunks - 1)
+                tile = chunk_of.index_select(0, u) * n_slices + sl
+                del deg, before, chunk_of
+            else:
+                tile = sl
+            key = tile * nu + u
+            del sl, i
+            _, order = torch.sort(key, stable=True)
+            del key, u
+            counts = torch.bincount(tile, minlength=n_chunks * n_slices)
+            offs = np.zeros(n_chunks * n_slices + 1, np.int64)
+            offs[1:] = torch.cumsum(counts, 0).cpu().numpy()
+            return order, offs
 
     def _dev(self, a, shape) -> torch.Tensor:
         if isinstance(a, torch.Tensor):
