@@ -244,6 +244,8 @@ class KernelMF(RecommenderBase):
         state.pop("_pred_engine", None)
         state.pop("_pred_key", None)
         state.pop("_param_ids", None)
+        state.pop("_maps_pending", None)
+        state.pop("_defer_maps", None)
         return state
 
     def __setstate__(self, state):
@@ -260,7 +262,20 @@ class KernelMF(RecommenderBase):
     def fit(self, X: pd.DataFrame, y: pd.Series):
         """kernel_matrix_factorization.py:81-128 (RNG: sample, normal(P),
         normal(Q), then one draw per epoch)."""
-        X = self._preprocess_data(X=X, y=y, type="fit")
+        # the user id map may be built on a worker thread beside the rest of
+        # fit() (RecommenderBase._fit_maps_native); joined before fit returns
+        self._defer_maps = True
+        try:
+            X = self._preprocess_data(X=X, y=y, type="fit")
+        finally:
+            self._defer_maps = False
+        try:
+            return self._fit_prepared(X)
+        finally:
+            self._join_maps()
+
+    def _fit_prepared(self, X: pd.DataFrame):
+        """fit() after _preprocess_data: initial draws, device epochs."""
         self.global_mean = X["rating"].mean()
         self.user_biases = np.zeros(self.n_users)
         self.item_biases = np.zeros(self.n_items)

@@ -11,7 +11,7 @@ the same calls gives the reference's results.
 from __future__ import annotations
 
 from abc import ABCMeta, abstractmethod
-from concurrent.futures import ThreadPoolExecutor
+from concurrent.futures import Future, ThreadPoolExecutor
 from typing import Any, Tuple, Union
 
 import numpy as np
@@ -23,6 +23,15 @@ from . import _prep
 # integer id columns of at least this many rows take the native
 # preprocessing path (mf_prep.cpp); results are identical either way
 FAST_PREP_MIN_ROWS = 1 << 16
+
+# one worker for id maps built beside fit()'s device work
+_MAP_POOL = ThreadPoolExecutor(1, thread_name_prefix="mf-idmap")
+
+
+def _id_map(uniq: np.ndarray) -> dict:
+    """{id: position} in first-appearance order (recommender_base.py:135-138:
+    ``{uid: n for n, uid in enumerate(unique)}``, NumPy scalar keys)."""
+    return dict(zip(uniq, range(len(uniq))))
 
 
 def _index_of(keys) -> pd.Index:
@@ -162,6 +171,13 @@ class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
             return out, known_users, new_users
         return out
 
+    def _join_maps(self) -> None:
+        """Wait for a user id map built on a worker thread (see
+        _fit_maps_native) and install it."""
+        fut = self.__dict__.pop("_maps_pending", None)
+        if fut is not None:
+            self.user_id_map = fut.result()
+
     def _int64_ids(self, X: pd.DataFrame):
         """(user ids, item ids) as int64 arrays when both columns are integer
         and the frame is large enough for the native path, else None."""
@@ -206,16 +222,29 @@ class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
             fut = [ex.submit(_prep.factorize_shuffled, d, perm) for d in dense[::-1]][::-1]
             num = rating.dtype.kind in "fiu"
             rfut = ex.submit(_prep.gather, rating, perm) if num else None
-            maps, codes = [None, None], [None, None]
+            maps, codes, sizes = [None, None], [None, None], [0, 0]
+            defer = getattr(self, "_defer_maps", False)
             for k in (1, 0):
                 c, uniq = fut[k].result()
                 dt = self._id_dtypes[k]
                 uniq = uniq.view(dt) if dt.itemsize == 8 else uniq.astype(dt)
-                maps[k] = dict(zip(uniq, range(len(uniq))))
+                sizes[k] = len(uniq)
+                if defer and k == 0:
+                    # the user map (10^6 entries at C3, ~0.2 s of dict
+                    # inserts) is built on a worker thread while fit() goes
+                    # on; fit() joins it before it returns (_join_maps)
+                    maps[k] = _MAP_POOL.submit(_id_map, uniq)
+                else:
+                    maps[k] = _id_map(uniq)
                 codes[k] = c
             rating = rfut.result() if num else rating[perm]
-        self.user_id_map, self.item_id_map = maps
-        self.n_users, self.n_items = len(maps[0]), len(maps[1])
+        if isinstance(maps[0], Future):
+            self._maps_pending = maps[0]
+            self.user_id_map = None
+        else:
+            self.user_id_map = maps[0]
+        self.item_id_map = maps[1]
+        self.n_users, self.n_items = sizes
         idx = index
         if isinstance(idx, pd.RangeIndex):
             idx = pd.Index(idx.start + idx.step * perm if (idx.start, idx.step) != (0, 1)

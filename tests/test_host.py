@@ -238,8 +238,10 @@ def cpu_engine(monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["tiny_linear", "tiny_sigmoid", "tiny_rbf", "tiny_defaults",
-                                  "mid_k100"])
+                                  "mid_k100", "c1_linear"])
 def test_kernelmf_host_flow_matches_reference(cpu_engine, name, capsys):
+    # c1_linear (80K ratings >= FAST_PREP_MIN_ROWS) takes the native
+    # preprocessing path, its user id map built beside the epochs
     from matrix_factorization import KernelMF
 
     d = load_golden(name)
