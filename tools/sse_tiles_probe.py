@@ -2,8 +2,8 @@
 """Time the training-SSE pass (mf_sse) at C3 over evaluation tilings:
 user chunks x item slices (mf_sched_tiles), walked in phases by a resident
 grid (k_sse_phased) or, with a trailing 'd', by the dispatch-ordered grid.
-Usage: python tools/sse_tiles_probe.py [--dtype float64] C,S[d] ...
-(1,8 = the round-5 default evaluation order)"""
+Usage: python tools/sse_tiles_probe.py [--dtype float64] CxS[d] ...
+(1x8 = the round-5 default evaluation order)"""
 
 import argparse
 import os
@@ -24,12 +24,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dtype", default="float64")
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("tiles", nargs="*", default=["1,8"])
+    ap.add_argument("tiles", nargs="*", default=["1x8"])
     args = ap.parse_args()
     nu, ni, nnz, k = 1_000_000, 100_000, 100_000_000, 64
     u, i, r = bench.synth(nu, ni, nnz)
     dt = args.dtype
-    os.environ["MF_SSE_TILES"] = args.tiles[0].rstrip("d")
+    os.environ["MF_SSE_TILES"] = args.tiles[0].rstrip("d").replace("x", ",")
     eng = SGDEngine(u, i, r, nu, ni, k, "linear", dt, "cuda:0",
                     global_mean=float(r.mean()), min_rating=1, max_rating=5)
     rs = np.random.RandomState(0)
@@ -38,7 +38,7 @@ def main():
                     np.zeros(nu, dt), np.zeros(ni, dt))
     ref = None
     for t in args.tiles:
-        os.environ["MF_SSE_TILES"] = t.rstrip("d")
+        os.environ["MF_SSE_TILES"] = t.rstrip("d").replace("x", ",")
         os.environ["MF_SSE_PHASED"] = "0" if t.endswith("d") else "1"
         eng._build_eval()
         for _ in range(3):
