@@ -173,7 +173,9 @@ template <typename E>
 void shuffle_raw_2t(MT& mt, E* data, int64_t n) {
     if (n < 2) return;
     const int64_t total = n - 1;
-    constexpr int64_t kR = 1 << 16, kChunk = 1 << 11, kAhead = 48;
+    constexpr int64_t kR = 1 << 16, kChunk = 1 << 11;
+    const char* ea = std::getenv("MF_SHUFFLE_AHEAD");           // probes
+    const int64_t kAhead = ea ? std::max(1, std::min(8192, std::atoi(ea))) : 256;
     std::unique_ptr<uint32_t[]> ring(new uint32_t[kR]);
     alignas(64) std::atomic<int64_t> drawn{0};
     alignas(64) std::atomic<int64_t> done{0};
@@ -225,14 +227,16 @@ void shuffle_raw_2t(MT& mt, E* data, int64_t n) {
     swapper.join();
 }
 
-// shuffle_raw, on two threads from this many elements (MF_SHUFFLE_THREADS=1
-// keeps one)
+// shuffle_raw, or with MF_SHUFFLE_THREADS=2 shuffle_raw_2t from this many
+// elements.  One thread is the default: on the GPU box's host the two-thread
+// form measured SLOWER at 100M (0.44-0.58 vs 0.32-0.38 s; 1.1 vs 1.95 s in
+// the build container), profiles/r06/shuffle_time_{1thread,2threads}_r06c3.txt
 constexpr int64_t kShuffle2tMin = 1 << 22;
 
 template <typename E>
 void shuffle_any(MT& mt, E* data, int64_t n) {
     const char* env = std::getenv("MF_SHUFFLE_THREADS");
-    if (n >= kShuffle2tMin && !(env && env[0] == '1'))
+    if (n >= kShuffle2tMin && env && env[0] == '2')
         shuffle_raw_2t(mt, data, n);
     else
         shuffle_raw(mt, data, n);

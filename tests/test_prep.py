@@ -47,15 +47,15 @@ def test_legacy_shuffle_mid_stream():
         assert np.array_equal(a, b) and np.array_equal(x1, x2), draws
 
 
-@pytest.mark.parametrize("threads", [None, "1"])
+@pytest.mark.parametrize("threads", [None, "2"])
 @pytest.mark.parametrize("dtype,n,draws", [(np.int32, 5_000_000, 0), (np.int32, 4_194_305, 623),
                                            (np.int64, 4_500_001, 624), (np.int32, 6_000_011, 5)])
 def test_large_shuffle_is_numpys(dtype, n, draws, threads, monkeypatch):
     """Millions of elements (the prefetch ring wraps many times, the MT state
     crosses thousands of 624-word blocks): the same permutation and the same
     RandomState afterwards as np.random.shuffle, from any MT position -- on
-    the two-thread form (draws / swaps, the default from 2^22 elements) and
-    on one thread (MF_SHUFFLE_THREADS=1)."""
+    one thread (the default) and on the two-thread form (draws / swaps,
+    MF_SHUFFLE_THREADS=2)."""
     if threads is None:
         monkeypatch.delenv("MF_SHUFFLE_THREADS", raising=False)
     else:
@@ -73,7 +73,7 @@ def test_large_shuffle_is_numpys(dtype, n, draws, threads, monkeypatch):
     assert np.array_equal(a, b) and np.array_equal(x1, x2)
 
 
-@pytest.mark.parametrize("threads", [None, "1"])
+@pytest.mark.parametrize("threads", [None, "2"])
 def test_large_permutation_is_numpys(threads, monkeypatch):
     """np.random.permutation(n) at 5M (fit()'s X.sample(frac=1) draw), both
     shuffle forms: the same permutation and RandomState afterwards."""
