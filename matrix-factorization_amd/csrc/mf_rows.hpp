@@ -748,7 +748,14 @@ __global__ __launch_bounds__(kBlock) void k_sse_owned(ReadArgs<T> A, SliceTab SL
 //    of an error zeroed on idle slots and on non-lead lanes.
 // The walk of k_sse_lean over one wave's share [b0, b1) of the evaluation
 // order; returns the lane's part of the FP64 SSE (non-lead lanes: 0).
-template <typename T, int W, int GS, int V, int KERN, int S, bool U24>
+// BC (bias per chunk): the item and user biases of a chunk's GS ratings are
+// loaded ONE per lane when the chunk starts (lane l holds rating c + l's) and
+// handed to each rating's step by the same lane broadcast as its rating --
+// instead of one wave-wide load per rating and step (S + the user-change
+// loads per step: FP32 rank 64 issued as many bias loads as row loads,
+// 16 + 16 per step), which cost the texture path (TA) an instruction each
+// for 8 or 4 bytes.  Same values, same arithmetic, bit for bit.
+template <typename T, int W, int GS, int V, int KERN, int S, bool U24, bool BC = true>
 __device__ __forceinline__ double sse_lean_range(const ReadArgs<T>& A, int64_t b0, int64_t b1) {
     using VT = typename VecOf<T, W>::type;
     constexpr int R = kWave / GS;
@@ -800,6 +807,13 @@ __device__ __forceinline__ double sse_lean_range(const ReadArgs<T>& A, int64_t b
             for (int64_t c = 0; c < maxrun; c += GS) {
                 const int tu = nu_, ti = ni_;
                 const T tr = nr_;
+                // BC: the chunk's biases, one per lane (issued before the
+                // prefetch: the counter waits for them do not wait for it)
+                [[maybe_unused]] T tbi = (T)0, tbu = (T)0;
+                if constexpr (BC && KERN != MF_RBF) {
+                    tbi = buf_ld<0, T>(rbi, (uint32_t)ti * (uint32_t)sizeof(T));
+                    tbu = buf_ld<0, T>(rbu, (uint32_t)tu * (uint32_t)sizeof(T));
+                }
                 if (c + GS < maxrun) fetch(c + GS, nu_, ni_, nr_);      // prefetch
 #pragma unroll 1
                 for (int t = 0; t < GS; t += S) {
@@ -826,8 +840,12 @@ __device__ __forceinline__ double sse_lean_range(const ReadArgs<T>& A, int64_t b
                             const int vc = FULL || vi < kv ? vi : kv - 1;
                             q[x][v] = buf_ld<0, VT>(rq, row_off(ii[x], vc));
                         }
-                        if constexpr (KERN != MF_RBF)
-                            bi[x] = buf_ld<0, T>(rbi, (uint32_t)ii[x] * (uint32_t)sizeof(T));
+                        if constexpr (KERN != MF_RBF) {
+                            if constexpr (BC)
+                                bi[x] = take_f<GS>(tbi, g * GS + t + x);
+                            else
+                                bi[x] = buf_ld<0, T>(rbi, (uint32_t)ii[x] * (uint32_t)sizeof(T));
+                        }
                         // wave-uniform: skipped unless some group changes user
                         // here; a lane that keeps its user reads out of range
                         if (__builtin_amdgcn_ballot_w64(need[x]) != 0) {
@@ -837,10 +855,11 @@ __device__ __forceinline__ double sse_lean_range(const ReadArgs<T>& A, int64_t b
                                 const int vc = FULL || vi < kv ? vi : kv - 1;
                                 pl[x][v] = buf_ld<0, VT>(rp, need[x] ? row_off(uu[x], vc) : kBufDropRd);
                             }
-                            if constexpr (KERN != MF_RBF)
+                            if constexpr (KERN != MF_RBF && !BC)
                                 bul[x] = buf_ld<0, T>(rbu, need[x] ? (uint32_t)uu[x] * (uint32_t)sizeof(T)
                                                                    : kBufDropRd);
                         }
+                        if constexpr (KERN != MF_RBF && BC) bul[x] = take_f<GS>(tbu, g * GS + t + x);
                     }
 #pragma unroll
                     for (int x = 0; x < S; ++x) {
@@ -888,13 +907,13 @@ __device__ __forceinline__ void sse_block_partial(double acc, double* partials) 
     }
 }
 
-template <typename T, int W, int GS, int V, int KERN, int S, bool U24>
+template <typename T, int W, int GS, int V, int KERN, int S, bool U24, bool BC = true>
 __global__ __launch_bounds__(kBlock) void k_sse_lean(ReadArgs<T> A, SliceTab SL) {
     const SliceWave sw = slice_wave(SL);
     const int64_t s0 = SL.off[sw.x], len = SL.off[sw.x + 1] - s0;
     const int64_t b0 = s0 + len * sw.wv / sw.nw;
     const int64_t b1 = s0 + len * (sw.wv + 1) / sw.nw;
-    sse_block_partial(sse_lean_range<T, W, GS, V, KERN, S, U24>(A, b0, b1), A.partials);
+    sse_block_partial(sse_lean_range<T, W, GS, V, KERN, S, U24, BC>(A, b0, b1), A.partials);
 }
 
 // Training SSE over TILES walked in phases by a resident grid (the FP64
@@ -1291,6 +1310,13 @@ struct SseRun {
                  : u24      ? k_sse_lean<T, W, GS, V, KERN, S, true>
                             : k_sse_lean<T, W, GS, V, KERN, S, false>;
         if (var == 0 && ev && std::atoi(ev) == 6) { var = 6; kfn = k_sse_owned<T, W, GS, V, KERN, S>; }
+        // probe: 12 = the round-5 k_sse_lean (a bias load per rating and step)
+        if (var == 0 && u24 && ev && std::atoi(ev) == 12) {
+            var = 12;
+            kfn = k_sse_lean<T, W, GS, V, KERN, S, true, false>;
+            if constexpr (GS == 16 && V == 1 && std::is_same<T, float>::value)
+                kfn = k_sse_lean<T, W, GS, V, KERN, 16, true, false>;
+        }
         // FP32 rows of one vector per lane (rank 64): a whole chunk of 16
         // ratings per group per step (C3: 2.45 vs 2.52 ms with S = 4, 2.46
         // with 8; tools/sse_probe.py).  Probes: 2 = 8 per step, 3 = SlotsFor.
@@ -1319,7 +1345,7 @@ struct SseRun {
                           : k_sse_phased<T, W, GS, V, KERN, 16, false>;
         }
         if (var == 0 && !u24) var = 7;                    // its own occupancy entry
-        static int resident_tab[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // per instantiation and variant
+        static int resident_tab[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};   // per instantiation and variant
         int& resident = resident_tab[var];
         if (resident == 0) {
             const LaunchTrace lt;

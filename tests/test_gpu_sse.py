@@ -1,6 +1,7 @@
 """The training-RMSE pass (mf_sse, _calculate_rmse kernel_matrix_factorization.py:
-240-317) in its kernel variants: k_sse_lean (the default), k_sse_owned (user
-rows owned per run; variant 6),
+240-317) in its kernel variants: k_sse_lean (the default: biases loaded once
+per chunk), its round-5 form with a bias load per rating (variant 12),
+k_sse_owned (user rows owned per run; variant 6),
 k_sse_pipe (the same walk software-pipelined, pieces of 8 or 4 ratings) and
 k_sse_stream.  Per rating the arithmetic is identical; the FP64 sums differ
 only in accumulation order (the grid follows each kernel's occupancy), so
@@ -33,7 +34,7 @@ def test_sse_variants_agree(k, nu, ni, nnz, monkeypatch):
                     global_mean=float(r.mean()), min_rating=1, max_rating=5)
     eng.load_params(P, Q, bu, bi)
     got = {}
-    for slot, var in enumerate(("0", "4", "5", "1", "6")):
+    for slot, var in enumerate(("0", "4", "5", "1", "6", "12")):
         monkeypatch.setenv("MF_SSE_VARIANT", var)
         eng.sse_async(slot)
         got[var] = eng.sse_values(slot + 1)[slot]
