@@ -33,6 +33,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <functional>
+#include <immintrin.h>
 #include <memory>
 #include <thread>
 #include <vector>
@@ -117,6 +118,104 @@ inline uint32_t mt_temper(uint32_t y) {
     return y;
 }
 
+// ---- AVX-512 form of the draws (x86-64 hosts that have it; runtime check)
+// The twist 16 words at a time, the tempering 16 outputs at a time, and the
+// rejection of 16 outputs against the CURRENT bound at once: output k of a
+// chunk is really tested against bound - (accepted before it), which can
+// differ from the chunk's bound only for outputs within 16 of it, so a chunk
+// with such an output (or a mask change, the draws' end, or the ring's end
+// inside it) is done one output at a time instead -- the same outputs
+// consumed, the same targets, the same MT position as the scalar loop.
+__attribute__((target("avx512f"))) static inline __m512i mt_step16(__m512i cur, __m512i nxt,
+                                                                     __m512i far) {
+    const __m512i y = _mm512_or_si512(_mm512_and_si512(cur, _mm512_set1_epi32((int)kUpper)),
+                                      _mm512_and_si512(nxt, _mm512_set1_epi32((int)kLower)));
+    const __m512i one = _mm512_set1_epi32(1);
+    const __m512i mag = _mm512_maskz_mov_epi32(_mm512_test_epi32_mask(y, one),
+                                               _mm512_set1_epi32((int)kMatrixA));
+    return _mm512_xor_si512(_mm512_xor_si512(far, _mm512_srli_epi32(y, 1)), mag);
+}
+
+__attribute__((target("avx512f"))) static void mt_regen_512(MT& mt) {
+    uint32_t* key = mt.key;
+    int i = 0;
+    for (; i + 16 <= kN - kM; i += 16)                   // key[i + kM] not yet rewritten
+        _mm512_storeu_si512(key + i, mt_step16(_mm512_loadu_si512(key + i),
+                                               _mm512_loadu_si512(key + i + 1),
+                                               _mm512_loadu_si512(key + i + kM)));
+    for (; i < kN - kM; ++i) {
+        const uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
+        key[i] = key[i + kM] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+    }
+    for (; i + 16 <= kN - 1; i += 16)                    // key[i - (kN - kM)] already new
+        _mm512_storeu_si512(key + i, mt_step16(_mm512_loadu_si512(key + i),
+                                               _mm512_loadu_si512(key + i + 1),
+                                               _mm512_loadu_si512(key + i + (kM - kN))));
+    for (; i < kN - 1; ++i) {
+        const uint32_t y = (key[i] & kUpper) | (key[i + 1] & kLower);
+        key[i] = key[i + (kM - kN)] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+    }
+    const uint32_t y = (key[kN - 1] & kUpper) | (key[0] & kLower);
+    key[kN - 1] = key[kM - 1] ^ (y >> 1) ^ (-(y & 1u) & kMatrixA);
+    mt.pos = 0;
+}
+
+__attribute__((target("avx512f"))) static inline __m512i mt_temper16(__m512i y) {
+    y = _mm512_xor_si512(y, _mm512_srli_epi32(y, 11));
+    y = _mm512_xor_si512(y, _mm512_and_si512(_mm512_slli_epi32(y, 7),
+                                             _mm512_set1_epi32((int)0x9d2c5680u)));
+    y = _mm512_xor_si512(y, _mm512_and_si512(_mm512_slli_epi32(y, 15),
+                                             _mm512_set1_epi32((int)0xefc60000u)));
+    return _mm512_xor_si512(y, _mm512_srli_epi32(y, 18));
+}
+
+// the draws of one MT block from position p: targets into ring[d & (R-1)],
+// each prefetched; returns with p at the block's end or d at total
+template <typename E>
+__attribute__((target("avx512f"))) static void mt_draws_512(MT& mt, int& p, int64_t& d,
+                                                            uint32_t& maxv, int64_t total,
+                                                            uint32_t* ring, int64_t R,
+                                                            E* data) {
+    while (p < kN && d < total) {
+        if ((p & 15) == 0 && maxv >= 64 && d + 16 < total && (d & (R - 1)) + 16 <= R &&
+            __builtin_clz(maxv) == __builtin_clz(maxv - 16)) {
+            const uint32_t mask = 0xffffffffu >> __builtin_clz(maxv);
+            const __m512i v = _mm512_and_si512(mt_temper16(_mm512_loadu_si512(mt.key + p)),
+                                               _mm512_set1_epi32((int)mask));
+            const __mmask16 acc = _mm512_cmple_epu32_mask(v, _mm512_set1_epi32((int)maxv));
+            const __mmask16 risky =
+                _mm512_mask_cmpgt_epu32_mask(acc, v, _mm512_set1_epi32((int)(maxv - 16)));
+            if (!risky) {
+                uint32_t* o = ring + (d & (R - 1));
+                _mm512_mask_compressstoreu_epi32(o, acc, v);
+                const int na = __builtin_popcount((unsigned)acc);
+                for (int q = 0; q < na; ++q) __builtin_prefetch(data + o[q], 1, 1);
+                d += na;
+                maxv -= (uint32_t)na;
+                p += 16;
+                continue;
+            }
+        }
+        // one output, as the scalar loop
+        const uint32_t mask = 0xffffffffu >> __builtin_clz(maxv);
+        const uint32_t v = mt_temper(mt.key[p++]) & mask;
+        const uint32_t a = v <= maxv ? 1u : 0u;
+        ring[d & (R - 1)] = v;
+        __builtin_prefetch(data + v, 1, 1);
+        d += a;
+        maxv -= a;
+    }
+}
+
+bool use_avx512() {
+    static const bool cpu = [] {
+        __builtin_cpu_init();
+        return __builtin_cpu_supports("avx512f") != 0;
+    }();
+    const char* env = std::getenv("MF_SHUFFLE_SIMD");        // 0: the scalar draws
+    return cpu && !(env && env[0] == '0');
+}
+
 // NumPy's _shuffle_raw on x[0..n): for i = n-1 .. 1, swap x[i] with
 // x[random_interval(i)].  The draws do not depend on the data, so they are
 // made a block of MT outputs at a time, ahead of the swaps that use them
@@ -133,8 +232,17 @@ void shuffle_raw(MT& mt, E* data, int64_t n) {
     constexpr int64_t kR = 2048, kAhead = 64;        // target ring; swaps this far behind
     uint32_t ring[kR];
     int64_t drawn = 0, done = 0;
+    const bool simd = use_avx512();
     while (done < total) {
-        if (drawn < total) {                         // the rest of one MT block
+        if (drawn < total && simd) {                 // the rest of one MT block (AVX-512)
+            if (mt.pos == kN) mt_regen_512(mt);
+            int p = mt.pos;
+            uint32_t maxv = (uint32_t)(total - drawn);
+            int64_t d = drawn;
+            mt_draws_512(mt, p, d, maxv, total, ring, kR, data);
+            mt.pos = p;
+            drawn = d;
+        } else if (drawn < total) {                  // the rest of one MT block
             if (mt.pos == kN) mt.regen();
             int p = mt.pos;
             uint32_t maxv = (uint32_t)(total - drawn);   // bound of draw `drawn`: i = n-1-drawn

@@ -47,15 +47,21 @@ def test_legacy_shuffle_mid_stream():
         assert np.array_equal(a, b) and np.array_equal(x1, x2), draws
 
 
+@pytest.mark.parametrize("simd", [None, "0"])
 @pytest.mark.parametrize("threads", [None, "2"])
 @pytest.mark.parametrize("dtype,n,draws", [(np.int32, 5_000_000, 0), (np.int32, 4_194_305, 623),
                                            (np.int64, 4_500_001, 624), (np.int32, 6_000_011, 5)])
-def test_large_shuffle_is_numpys(dtype, n, draws, threads, monkeypatch):
+def test_large_shuffle_is_numpys(dtype, n, draws, threads, simd, monkeypatch):
     """Millions of elements (the prefetch ring wraps many times, the MT state
     crosses thousands of 624-word blocks): the same permutation and the same
     RandomState afterwards as np.random.shuffle, from any MT position -- on
     one thread (the default) and on the two-thread form (draws / swaps,
-    MF_SHUFFLE_THREADS=2)."""
+    MF_SHUFFLE_THREADS=2), with the AVX-512 draws where the host has them
+    and with the scalar draws (MF_SHUFFLE_SIMD=0)."""
+    if simd is None:
+        monkeypatch.delenv("MF_SHUFFLE_SIMD", raising=False)
+    else:
+        monkeypatch.setenv("MF_SHUFFLE_SIMD", simd)
     if threads is None:
         monkeypatch.delenv("MF_SHUFFLE_THREADS", raising=False)
     else:
