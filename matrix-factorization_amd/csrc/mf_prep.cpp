@@ -175,7 +175,7 @@ template <typename E>
 __attribute__((target("avx512f"))) static void mt_draws_512(MT& mt, int& p, int64_t& d,
                                                             uint32_t& maxv, int64_t total,
                                                             uint32_t* ring, int64_t R,
-                                                            E* data) {
+                                                            E* data, bool pf_draw) {
     while (p < kN && d < total) {
         if ((p & 15) == 0 && maxv >= 64 && d + 16 < total && (d & (R - 1)) + 16 <= R &&
             __builtin_clz(maxv) == __builtin_clz(maxv - 16)) {
@@ -189,7 +189,8 @@ __attribute__((target("avx512f"))) static void mt_draws_512(MT& mt, int& p, int6
                 uint32_t* o = ring + (d & (R - 1));
                 _mm512_mask_compressstoreu_epi32(o, acc, v);
                 const int na = __builtin_popcount((unsigned)acc);
-                for (int q = 0; q < na; ++q) __builtin_prefetch(data + o[q], 1, 1);
+                if (pf_draw)
+                    for (int q = 0; q < na; ++q) __builtin_prefetch(data + o[q], 1, 1);
                 d += na;
                 maxv -= (uint32_t)na;
                 p += 16;
@@ -201,7 +202,7 @@ __attribute__((target("avx512f"))) static void mt_draws_512(MT& mt, int& p, int6
         const uint32_t v = mt_temper(mt.key[p++]) & mask;
         const uint32_t a = v <= maxv ? 1u : 0u;
         ring[d & (R - 1)] = v;
-        __builtin_prefetch(data + v, 1, 1);
+        if (pf_draw) __builtin_prefetch(data + v, 1, 1);
         d += a;
         maxv -= a;
     }
@@ -229,17 +230,21 @@ template <typename E>
 void shuffle_raw(MT& mt, E* data, int64_t n) {
     if (n < 2) return;
     const int64_t total = n - 1;                     // draws, for i = n-1 .. 1
-    constexpr int64_t kR = 2048, kAhead = 64;        // target ring; swaps this far behind
+    constexpr int64_t kR = 2048, kAhead = 128;       // target ring; swaps this far behind
     uint32_t ring[kR];
     int64_t drawn = 0, done = 0;
     const bool simd = use_avx512();
+    // AVX-512 draws come in bursts of a block: their targets are prefetched
+    // by the swap loop kPf swaps ahead (MF_SHUFFLE_PF: 0 = at draw time)
+    const char* epf = std::getenv("MF_SHUFFLE_PF");
+    const int64_t kPf = simd ? (epf ? std::max(0, std::min(120, std::atoi(epf))) : 64) : 0;
     while (done < total) {
         if (drawn < total && simd) {                 // the rest of one MT block (AVX-512)
             if (mt.pos == kN) mt_regen_512(mt);
             int p = mt.pos;
             uint32_t maxv = (uint32_t)(total - drawn);
             int64_t d = drawn;
-            mt_draws_512(mt, p, d, maxv, total, ring, kR, data);
+            mt_draws_512(mt, p, d, maxv, total, ring, kR, data, kPf == 0);
             mt.pos = p;
             drawn = d;
         } else if (drawn < total) {                  // the rest of one MT block
@@ -262,6 +267,7 @@ void shuffle_raw(MT& mt, E* data, int64_t n) {
         }
         const int64_t lim = drawn < total ? drawn - kAhead : total;
         for (; done < lim; ++done) {
+            if (kPf && done + kPf < drawn) __builtin_prefetch(data + ring[(done + kPf) & (kR - 1)], 1, 1);
             const int64_t i = total - done;
             const int64_t j = ring[done & (kR - 1)];
             const E t = data[i];
