@@ -230,14 +230,14 @@ template <typename E>
 void shuffle_raw(MT& mt, E* data, int64_t n) {
     if (n < 2) return;
     const int64_t total = n - 1;                     // draws, for i = n-1 .. 1
-    constexpr int64_t kR = 2048, kAhead = 128;       // target ring; swaps this far behind
+    constexpr int64_t kR = 2048, kAhead = 256;       // target ring; swaps this far behind
     uint32_t ring[kR];
     int64_t drawn = 0, done = 0;
     const bool simd = use_avx512();
     // AVX-512 draws come in bursts of a block: their targets are prefetched
     // by the swap loop kPf swaps ahead (MF_SHUFFLE_PF: 0 = at draw time)
     const char* epf = std::getenv("MF_SHUFFLE_PF");
-    const int64_t kPf = simd ? (epf ? std::max(0, std::min(120, std::atoi(epf))) : 64) : 0;
+    const int64_t kPf = simd ? (epf ? std::max(0, std::min(248, std::atoi(epf))) : 128) : 0;
     while (done < total) {
         if (drawn < total && simd) {                 // the rest of one MT block (AVX-512)
             if (mt.pos == kN) mt_regen_512(mt);

@@ -1976,7 +1976,9 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
             exact_spare = np.empty_like(order)
 
             def shuffled_copy(src, dst):
-                np.copyto(dst, src)
+                # (torch's CPU copy is threaded: 400 MB at C3 in ~10 ms
+                # instead of np.copyto's ~40 ms on the worker's critical path)
+                torch.from_numpy(dst).copy_(torch.from_numpy(src))
                 _prep.legacy_shuffle_(dst)
                 return dst
     elif schedule == "colored":
