@@ -744,12 +744,16 @@ class SGDEngine:
             else:
                 tile = sl
             key = tile * nu + u
-            del sl, i
-            _, order = torch.sort(key, stable=True)
+            del sl, i, tile
+            skey, order = torch.sort(key, stable=True)
             del key, u
-            counts = torch.bincount(tile, minlength=n_chunks * n_slices)
-            offs = np.zeros(n_chunks * n_slices + 1, np.int64)
-            offs[1:] = torch.cumsum(counts, 0).cpu().numpy()
+            # tile t starts at the first key >= t * n_users (a search in the
+            # sorted keys: a histogram of 10^8 ids into 8 bins is ~4 ms of
+            # atomics on one address each)
+            T = n_chunks * n_slices
+            edges = torch.arange(T + 1, dtype=torch.int64, device=skey.device) * nu
+            offs = torch.searchsorted(skey, edges).cpu().numpy().astype(np.int64)
+            offs[-1] = n
             return order, offs
 
     def _dev(self, a, shape) -> torch.Tensor:
