@@ -46,6 +46,12 @@ def test_bench_two_ranks_checks_itself(exchange):
     if exchange == "rotate":
         assert m["replay"]["bit_equal"]
         assert d["phases"]["ring_pass_ms_per_epoch"] > 0
+        # the delta exchange measured in the same job, nested
+        de = d["delta_exchange"]
+        assert de["exchange"] == "delta" and de["value"] > 0
+        assert de["multi_gpu"]["replicas_agree"]
+    else:
+        assert "delta_exchange" not in d
     assert d["roofline"]["frac"] > 0
     # the default line: FP64 (the reference's arithmetic) at top level, the
     # FP32 perf layout nested with its own checks
