@@ -530,48 +530,126 @@ struct MmArgs {
     const int32_t* probe;                // k_topk_mw: probe items (k_topk_probe), n_probe of them
     int32_t n_probe, probe_group;        // ... one per group of probe_group consecutive ids
     const bf16x8* Qs;                    // k_topk_mw<.., BF>: Q split into bf16 hi + lo (k_topk_split_q)
+    int32_t* big;                        // users left to k_topk_mm_merge by k_topk_mm_merge_wave
+    int32_t* n_big;                      // ... their count (null big: k_topk_mm_merge takes all)
 };
 
-// max item-row norm and max |b_i| (non-negative floats: integer max of the bits);
-// the blocks past the items': max query-user row norm into stats[2]
+// k_topk_mm_stats: max item-row norm and max |b_i| into stats[0..1], max
+// query-user row norm into stats[2].  Each wave reads 64-row chunks; where
+// k / 4 is a power of two (k = 4 .. 64) a row is read by L = k / 4 lanes,
+// one float4 each, so a wave load covers 64 / L whole rows, all L loads of
+// a chunk in flight before the group sums (round 6: one row per lane made
+// each load touch 64 lines, and with one atomic per wave on one word the
+// kernel took 57 us of the C3 top-k's 1.07 ms).  The norms only bound the
+// MFMA filter's error (with a 1e-4 safety factor): any summation order.
+__device__ __forceinline__ float row_norm_any(const float* row, int k) {
+    float s2 = 0.f;
+    for (int f = 0; f < k; ++f) s2 = __builtin_fmaf(row[f], row[f], s2);
+    return sqrtf(s2);
+}
+
+// the largest row norm of rows[0 .. 64) of a wave's chunk (row r < 0:
+// none), L = k / 4 lanes per row: all L loads issued before any sum
+template <int L>
+__device__ __forceinline__ float chunk_max_norm(const float* base, int k, const int64_t* rowv,
+                                                int lane) {
+    float4 v[L];
+    bool ok[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+        const int64_t row = rowv[j];
+        ok[j] = row >= 0;
+        v[j] = *reinterpret_cast<const float4*>(base + (ok[j] ? row : 0) * k + 4 * (lane % L));
+    }
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+        float s2 = v[j].x * v[j].x;
+        s2 = __builtin_fmaf(v[j].y, v[j].y, s2);
+        s2 = __builtin_fmaf(v[j].z, v[j].z, s2);
+        s2 = __builtin_fmaf(v[j].w, v[j].w, s2);
+#pragma unroll
+        for (int o = 1; o < L; o <<= 1) s2 += __shfl_xor(s2, o, kWave);
+        if (ok[j]) m = fmaxf(m, sqrtf(s2));
+    }
+    return m;
+}
+
+template <int L>
+__device__ __forceinline__ float chunk_norms(const float* base, int k, int64_t w0, int64_t n,
+                                             const int32_t* users, int lane) {
+    constexpr int per = kWave / L;
+    // users: one id per lane, handed to the lanes that read its row
+    const int32_t uid = users && w0 + lane < n ? users[w0 + lane] : -1;
+    int64_t rowv[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+        const int r = per * j + lane / L;
+        if (users) {
+            rowv[j] = __shfl(uid, r, kWave);
+        } else {
+            rowv[j] = w0 + r < n ? w0 + r : -1;
+        }
+    }
+    return chunk_max_norm<L>(base, k, rowv, lane);
+}
+
+// blocks [0, nb_items): item rows, the rest: query users; every wave strides
+// over 64-row chunks, one atomic per block and statistic (round 6: one per
+// wave on a single word was ~35 of the kernel's 57 us)
 __global__ __launch_bounds__(kBlock) void k_topk_mm_stats(const float* __restrict__ Q,
                                                           const float* __restrict__ Bi,
                                                           int32_t n_items, int32_t k,
                                                           float* stats,
                                                           const int32_t* __restrict__ users,
                                                           int32_t nq_users,
-                                                          const float* __restrict__ P) {
-    const int64_t nb_items = ((int64_t)n_items + kBlock - 1) / kBlock;
-    if ((int64_t)blockIdx.x >= nb_items) {
-        const int64_t q = ((int64_t)blockIdx.x - nb_items) * kBlock + threadIdx.x;
-        float pn = 0.f;
-        const int32_t uu = q < nq_users ? users[q] : -1;
-        if (uu >= 0) {
-            const float* pr = P + (int64_t)uu * k;
-            for (int f = 0; f < k; ++f) pn = __builtin_fmaf(pr[f], pr[f], pn);
-            pn = sqrtf(pn);
+                                                          const float* __restrict__ P,
+                                                          int32_t nb_items) {
+    __shared__ float s_red[2][kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const bool user_part = (int)blockIdx.x >= nb_items;
+    const int b = user_part ? (int)blockIdx.x - nb_items : (int)blockIdx.x;
+    const int nb = user_part ? (int)gridDim.x - nb_items : nb_items;
+    const int64_t n = user_part ? nq_users : n_items;
+    const float* base = user_part ? P : Q;
+    const int32_t* ids = user_part ? users : nullptr;
+    float m0 = 0.f, m1 = 0.f;                      // max norm, max |b_i|
+    for (int64_t w0 = ((int64_t)b * kWavesPerBlock + wv) * kWave; w0 < n;
+         w0 += (int64_t)nb * kWavesPerBlock * kWave) {
+        float m;
+        switch (k) {
+            case 64: m = chunk_norms<16>(base, k, w0, n, ids, lane); break;
+            case 32: m = chunk_norms<8>(base, k, w0, n, ids, lane); break;
+            case 16: m = chunk_norms<4>(base, k, w0, n, ids, lane); break;
+            case 8: m = chunk_norms<2>(base, k, w0, n, ids, lane); break;
+            case 4: m = chunk_norms<1>(base, k, w0, n, ids, lane); break;
+            default: {
+                m = 0.f;
+                const int64_t row = w0 + lane < n ? (ids ? ids[w0 + lane] : w0 + lane) : -1;
+                if (row >= 0) m = row_norm_any(base + row * k, k);
+            }
         }
-        for (int o = 32; o > 0; o >>= 1) pn = fmaxf(pn, __shfl_xor(pn, o, kWave));
-        if ((threadIdx.x & (kWave - 1)) == 0) atomicMax(reinterpret_cast<int*>(stats) + 2, __float_as_int(pn));
-        return;
+        m0 = fmaxf(m0, m);
+        if (!user_part && w0 + lane < n) m1 = fmaxf(m1, fabsf(Bi[w0 + lane]));
     }
-    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    float nq = 0.f, nb = 0.f;
-    if (i < n_items) {
-        const float* q = Q + i * k;
-        for (int f = 0; f < k; ++f) nq = __builtin_fmaf(q[f], q[f], nq);
-        nq = sqrtf(nq) * 1.0001f;
-        nb = fabsf(Bi[i]);
+    for (int o = 32; o > 0; o >>= 1) {
+        m0 = fmaxf(m0, __shfl_xor(m0, o, kWave));
+        m1 = fmaxf(m1, __shfl_xor(m1, o, kWave));
     }
-    nq = fmaxf(nq, __shfl_xor(nq, 32, kWave));
-    nb = fmaxf(nb, __shfl_xor(nb, 32, kWave));
-    for (int o = 16; o > 0; o >>= 1) {
-        nq = fmaxf(nq, __shfl_xor(nq, o, kWave));
-        nb = fmaxf(nb, __shfl_xor(nb, o, kWave));
-    }
-    if ((threadIdx.x & (kWave - 1)) == 0) {
-        atomicMax(reinterpret_cast<int*>(stats), __float_as_int(nq));
-        atomicMax(reinterpret_cast<int*>(stats) + 1, __float_as_int(nb));
+    if (lane == 0) { s_red[0][wv] = m0; s_red[1][wv] = m1; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int x = 1; x < kWavesPerBlock; ++x) {
+            m0 = fmaxf(m0, s_red[0][x]);
+            m1 = fmaxf(m1, s_red[1][x]);
+        }
+        // non-negative floats: integer max of the bits
+        if (user_part) {
+            atomicMax(reinterpret_cast<int*>(stats) + 2, __float_as_int(m0));
+        } else {
+            atomicMax(reinterpret_cast<int*>(stats), __float_as_int(m0 * 1.0001f));
+            atomicMax(reinterpret_cast<int*>(stats) + 1, __float_as_int(m1));
+        }
     }
 }
 
@@ -1053,6 +1131,22 @@ __device__ __forceinline__ float writelane_f(float x, int l, float v) {
                                                  __builtin_bit_cast(int, v)));
 }
 
+// the r-th largest (r >= 1, with multiplicity) of v over the lanes with m
+// set (at least r of them): a binary search on order-preserving keys, 32
+// ballots (round 6; was a rank count of every entry against every other,
+// one readlane pair per entry)
+__device__ __forceinline__ float wave_rth_largest(float v, bool m, int r) {
+    const uint32_t b = __float_as_uint(v);
+    const uint32_t key = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    uint32_t t = 0;
+    for (int bit = 31; bit >= 0; --bit) {
+        const uint32_t c = t | (1u << bit);
+        if (__popcll(__builtin_amdgcn_ballot_w64(m && key >= c)) >= r) t = c;
+    }
+    const uint64_t at = __builtin_amdgcn_ballot_w64(m && key == t);
+    return readlane_f(v, (int)__builtin_ctzll(at));
+}
+
 template <int SEG, bool PIPE = true, bool BF = false>
 __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
     constexpr int CAP = kMwCap;
@@ -1272,20 +1366,12 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
             }
             if (ex) { v = -INFINITY; it = 0x7fffffff; }
         }
-        // rank in (s' desc, id asc) among the entries
-        int rk = 0;
-        for (int j = 0; j < n; ++j) {
-            const float vj = readlane_f(v, j);
-            const int32_t ij = __builtin_amdgcn_readlane(it, j);
-            rk += (vj > v || (vj == v && ij < it)) ? 1 : 0;
-        }
+        // the rank-th best s' (the entry of rank - 1 in (s' desc, id asc))
         const bool val = v != -INFINITY;
         const int rank = A.amount + (check || probing ? 0 : extra);   // <= CAP - 32 (kMwMaxAmount)
         bound = -INFINITY;
-        if (__popcll(__builtin_amdgcn_ballot_w64(val)) >= rank) {
-            const uint64_t at = __builtin_amdgcn_ballot_w64(val && rk == rank - 1);
-            bound = readlane_f(v, (int)__builtin_ctzll(at)) - 2.f * s_m[m];
-        }
+        if (__popcll(__builtin_amdgcn_ballot_w64(val)) >= rank)
+            bound = wave_rth_largest(v, val, rank) - 2.f * s_m[m];
         bound = fmaxf(bound, readlane_f(lfloor, r));
         return __builtin_amdgcn_ballot_w64(val && v >= bound);
     };
@@ -1487,8 +1573,70 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
             if (lane + kWave * j < ntot) s_exw[lane + kWave * j] = val[j];
     }
     asm volatile("" ::: "memory");
-    load_b(ibeg);
-    if constexpr (PIPE) {
+    if constexpr (PIPE && BF) {
+        // Two operand sets (round 6): tile c+2 loads into the set tile c
+        // used, right after the first MFMA of tile c+1 -- a whole tile of
+        // MFMAs and admission work ahead of its use.  (With one set, the
+        // second half of tile c+2's operands could only load once tile
+        // c+1's last MFMA had read that half, i.e. at the step's end, and
+        // the next step waited for it.)
+        bf16x8 sh[2][NB], sl[2][NB];
+        float sb[2];
+        auto fetch_set = [&](int it0, int S) __attribute__((always_inline)) {
+            sb[S] = A.Bi[item_of(it0)];
+            const bf16x8* tb = tile_ptr(it0);
+#pragma unroll
+            for (int s2 = 0; s2 < NB; ++s2) {
+                sh[S][s2] = tb[(2 * s2) * 64 + lane];
+                sl[S][s2] = tb[(2 * s2 + 1) * 64 + lane];
+            }
+        };
+        auto mfma_s = [&](f32x16& x, int m, int S) __attribute__((always_inline)) {
+            const int s2 = m / 3, t = m % 3;
+            x = __builtin_amdgcn_mfma_f32_32x32x16_bf16(t == 0 ? al[s2] : ah[s2],
+                                                        t == 1 ? sl[S][s2] : sh[S][s2], x, 0, 0, 0);
+        };
+        f32x16 xa, xb;
+        fetch_set(ibeg, 0);
+        fetch_set(ibeg + 32, 1);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) xa[i] = 0.f;
+#pragma unroll
+        for (int m = 0; m < NM; ++m) mfma_s(xa, m, 0);
+        // x: tile c0 (its operands were set 1 - S), y: tile c0 + 32 from set S
+        auto step2 = [&](int c0, f32x16& x, f32x16& y, int S) __attribute__((always_inline)) {
+            const float bx = sb[1 - S];
+            const float mb = A.mu + bx;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) y[i] = 0.f;
+            const bool have = c0 + c < iend;
+            // the admission test of tile c0 as in `step` below (sign bits of
+            // sp - adm ANDed over the rows; the exact per-row test decides)
+            uint32_t neg = 0xffffffffu;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+#pragma unroll
+                for (int m = i * NM / 16; m < (i + 1) * NM / 16; ++m) mfma_s(y, m, S);
+                if (i == 1) fetch_set(c0 + 64, 1 - S);
+                const float sp = (mb + ubu[i]) + x[i];
+                neg &= __builtin_bit_cast(uint32_t, sp - uadm[i]);
+            }
+            if (__builtin_amdgcn_ballot_w64(have && !(neg >> 31))) {     // wave-uniform
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float sp = (mb + ubu[i]) + x[i];
+                    const uint64_t bal = __builtin_amdgcn_ballot_w64(have && sp >= uadm[i]);
+                    if (bal) insert_row(i, c0, x, bx, bal);
+                }
+            }
+            settle();
+        };
+        for (int c0 = ibeg; c0 < iend; c0 += 64) {
+            step2(c0, xa, xb, 1);
+            if (c0 + 32 < iend) step2(c0 + 32, xb, xa, 0);
+        }
+    } else if constexpr (PIPE) {
+        load_b(ibeg);
         // Tile c+1's MFMAs interleaved with tile c's admission, row by row:
         // the 16 accumulator rows of tile c are compared and inserted
         // between the SEG / 16 MFMAs of each slice of tile c+1, so the list
@@ -1516,16 +1664,22 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
             const bool have = c0 + c < iend;
             // admission test of tile c's rows between the MFMAs, one branch
             // per tile (a tile admits anything rarely once the floor is set:
-            // the per-row ballot and branch were most of the loop's issue)
-            bool anyl = false;
+            // the per-row ballot and branch were most of the loop's issue).
+            // Branch-free: the sign bits of sp - adm ANDed over the rows
+            // (sp >= adm <=> sp - adm >= +0 for finite sp, adm = +-inf
+            // included); a NaN only sends the tile to the exact per-row
+            // test below, which decides.
+            const float mb = A.mu + bx;
+            uint32_t neg = 0xffffffffu;
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
 #pragma unroll
                 for (int m = i * NM / 16; m < (i + 1) * NM / 16; ++m) mfma_m(y, m);
                 if (i == 7) load_half(c0 + 64, 0);       // tile c+2, columns of the first half
-                const float sp = ((A.mu + bx) + ubu[i]) + x[i];
-                anyl = anyl || (have && sp >= uadm[i]);
+                const float sp = (mb + ubu[i]) + x[i];
+                neg &= __builtin_bit_cast(uint32_t, sp - uadm[i]);
             }
+            const bool anyl = have && !(neg >> 31);
             if (__builtin_amdgcn_ballot_w64(anyl)) {     // wave-uniform
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
@@ -1542,6 +1696,7 @@ __global__ __launch_bounds__(kBlock) void k_topk_mw(MmArgs A) {
             if (c0 + 32 < iend) step(c0 + 32, xb, bb, xa, ba);
         }
     } else {
+        load_b(ibeg);
         for (int c0 = ibeg; c0 < iend; c0 += 32) {
             f32x16 acc;
             tile(acc);
@@ -1582,9 +1737,13 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm_merge(MmArgs A, int32_t* out
     __shared__ int32_t s_id[kMmMaxSplits * kMmCap];
     __shared__ uint64_t s_key[kMmMaxSplits * kMmCap];
     __shared__ int s_off[kMmMaxSplits + 1], s_keep;
-    const int qy = blockIdx.x, tid = threadIdx.x;
+    const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1), wv = tid / kWave;
     const int ns = A.n_splits;                       // <= kMmMaxSplits (topk_mm_splits)
+    // the users k_topk_mm_merge_wave listed (bands past 64 entries), or all
+    const int n_users = A.big ? *A.n_big : A.nq;
+    for (int xq = blockIdx.x; xq < n_users; xq += gridDim.x) {
+    const int qy = A.big ? A.big[xq] : xq;
     if (tid == 0) {
         int n = 0;
         for (int x = 0; x < ns; ++x) { s_off[x] = n; n += A.part_n[(int64_t)qy * ns + x]; }
@@ -1648,6 +1807,109 @@ __global__ __launch_bounds__(kBlock) void k_topk_mm_merge(MmArgs A, int32_t* out
         out_items[(int64_t)qy * A.amount + y] = ok ? s_id[y] : -1;
         out_scores[(int64_t)qy * A.amount + y] =
             ok ? (float)key_score(s_key[y]) : __int_as_float(0x7fc00000);
+    }
+    __syncthreads();                                 // the LDS lists are reused
+    }
+}
+
+// k_topk_mm_merge for the users whose bands hold at most 64 entries over
+// all splits (C3, top-10: ~18): one wave per user, entries one per lane, no
+// workgroup barrier (round 6; the workgroup-per-user form's two bitonic
+// sorts with a barrier per stage took 90 us of the C3 top-k's 1.07 ms).
+// Same keep rule (s' >= the amount-th best s' - 2M), the same rescoring
+// arithmetic and the same (key desc, id asc) order, so the same output;
+// users with more entries are listed for k_topk_mm_merge (A.big).
+template <int GS>
+__global__ __launch_bounds__(kBlock) void k_topk_mm_merge_wave(MmArgs A, int32_t* out_items,
+                                                               float* out_scores) {
+    __shared__ int32_t s_kid[kWavesPerBlock][kWave];
+    __shared__ uint64_t s_kkey[kWavesPerBlock][kWave];
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+    const int qy = blockIdx.x * kWavesPerBlock + wv;
+    if (qy >= A.nq) return;                              // wave-uniform
+    const int ns = A.n_splits;
+    // offsets of the splits' bands (inclusive scan over lanes < ns)
+    const int cnt = lane < ns ? A.part_n[(int64_t)qy * ns + lane] : 0;
+    int incl = cnt;
+    for (int o = 1; o < kMmMaxSplits; o <<= 1) {
+        const int t = __shfl_up(incl, o, kWave);
+        if (lane >= o) incl += t;
+    }
+    const int n = __builtin_amdgcn_readlane(incl, kMmMaxSplits - 1);
+    if (n > kWave) {                                     // k_topk_mm_merge's user
+        if (lane == 0) A.big[atomicAdd(A.n_big, 1)] = qy;
+        return;
+    }
+    float sc = -INFINITY;
+    int32_t id = 0x7fffffff;
+    const bool valid = lane < n;
+    int x = 0, base = 0;                                 // split of entry `lane`, its start
+    for (int t = 0; t < ns; ++t) {                       // wave-uniform
+        const int end = __builtin_amdgcn_readlane(incl, t);
+        if (lane >= end) { x = t + 1; base = end; }
+    }
+    if (valid) {
+        const int64_t o = ((int64_t)qy * ns + x) * kMmCap + (lane - base);
+        sc = A.part_s[o];
+        id = A.part_id[o];
+    }
+    uint64_t keep = __builtin_amdgcn_ballot_w64(valid);
+    if (n >= A.amount) {
+        // the amount-th best s' (the sorted list's entry amount - 1)
+        const float adm = wave_rth_largest(sc, valid, A.amount) - 2.f * A.marg[qy];
+        keep = __builtin_amdgcn_ballot_w64(valid && sc >= adm);
+    }
+    const int K = __popcll(keep);
+    const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(keep >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)keep, 0u));
+    if ((keep >> lane) & 1) s_kid[wv][pos] = id;
+    asm volatile("" ::: "memory");
+    // exact rescoring, R candidates per pass (k_topk_mm_merge's arithmetic)
+    const int32_t uu = A.users[qy];
+    const float bu = uu >= 0 ? A.Bu[uu] : 0.f;
+    const int k = A.k;
+    const int g = lane / GS, l = lane % GS;
+    constexpr int R = kWave / GS;
+    const float pl = (uu >= 0 && l < k) ? A.P[(int64_t)uu * k + l] : 0.f;
+    constexpr int U = 4;                                 // candidates' loads in flight
+    for (int y0 = 0; y0 < K; y0 += U * R) {              // wave-uniform
+        float ql[U], bq[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int y = y0 + u * R + g;
+            const bool have = y < K;
+            const int32_t it = have ? s_kid[wv][y] : 0;
+            ql[u] = (have && l < k) ? A.Q[(int64_t)it * k + l] : 0.f;
+            bq[u] = have ? A.Bi[it] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int y = y0 + u * R + g;
+            const float s2 = group_sum<GS>(0.f + pl * ql[u]);
+            const float pred = ((A.mu + bq[u]) + bu) + s2;
+            if (y < K && l == 0) s_kkey[wv][y] = order_key((double)pred);
+        }
+    }
+    asm volatile("" ::: "memory");
+    // (key desc, id asc) rank among the K kept, the first `amount` written
+    uint64_t key = 0;
+    int32_t kid = 0x7fffffff;
+    if (lane < K) { key = s_kkey[wv][lane]; kid = s_kid[wv][lane]; }
+    int rk = 0;
+    for (int j = 0; j < K; ++j) {
+        const uint64_t kj = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(key >> 32), j) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)key, j);
+        const int32_t ij = __builtin_amdgcn_readlane(kid, j);
+        rk += cand_before(kj, ij, key, kid) ? 1 : 0;
+    }
+    const int64_t ob = (int64_t)qy * A.amount;
+    if (lane < K && rk < A.amount) {
+        out_items[ob + rk] = kid;
+        out_scores[ob + rk] = (float)key_score(key);
+    }
+    for (int y = K + lane; y < A.amount; y += kWave) {
+        out_items[ob + y] = -1;
+        out_scores[ob + y] = __int_as_float(0x7fc00000);
     }
 }
 
@@ -1814,7 +2076,7 @@ extern "C" size_t mf_topk_mm_workspace_bytes(int32_t n_query, int32_t n_items) {
     const size_t ns = (size_t)std::max(topk_mm_splits(n_query, n_items),
                                        topk_mw_splits(n_query, n_items));
     return 16 + 4 * (size_t)n_query + 4 * (size_t)n_query * ns +
-           8 * (size_t)n_query * ns * kMmCap + 4 * (size_t)kMwProbe + 16 +
+           8 * (size_t)n_query * ns * kMmCap + 4 * (size_t)kMwProbe + 4 * (size_t)n_query + 16 +
            kMwSplitRowBytes * (32 * (((size_t)n_items + 31) / 32) + kMwProbe);
 }
 
@@ -1875,8 +2137,10 @@ extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double gl
     a.part_id = (int32_t*)(a.part_s + (size_t)n_query * a.n_splits * kMmCap);
     a.overflow = overflow;
     a.probe = (int32_t*)(a.part_id + (size_t)n_query * a.n_splits * kMmCap);
+    a.big = const_cast<int32_t*>(a.probe) + kMwProbe;
+    a.n_big = reinterpret_cast<int32_t*>(stats) + 3;    // zeroed with the statistics
     {
-        const uintptr_t qs = reinterpret_cast<uintptr_t>(a.probe + kMwProbe);
+        const uintptr_t qs = reinterpret_cast<uintptr_t>(a.big + n_query);
         a.Qs = reinterpret_cast<const bf16x8*>((qs + 15) & ~(uintptr_t)15);
     }
     const char* pe = std::getenv("MF_TOPK_MM_PIPE");
@@ -1897,10 +2161,10 @@ extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double gl
         a.fill = std::max(amount + 1, std::min(fv, kMwCap - 32));
     }
     MF_HIP_CHECK(hipMemsetAsync(stats, 0, 16, st));
-    const unsigned nb_stats = (unsigned)((n_items + kBlock - 1) / kBlock +
-                                         (a.n_probe > 0 ? (n_query + kBlock - 1) / kBlock : 0));
-    hipLaunchKernelGGL(k_topk_mm_stats, dim3(nb_stats), dim3(kBlock), 0, st, a.Q, a.Bi, n_items,
-                       n_factors, stats, query_users, n_query, a.P);
+    const int32_t nb_si = (int32_t)std::min<int64_t>(512, ((int64_t)n_items + kBlock - 1) / kBlock);
+    const int32_t nb_su = a.n_probe > 0 ? (int32_t)std::min<int64_t>(64, ((int64_t)n_query + kBlock - 1) / kBlock) : 0;
+    hipLaunchKernelGGL(k_topk_mm_stats, dim3((unsigned)(nb_si + nb_su)), dim3(kBlock), 0, st, a.Q,
+                       a.Bi, n_items, n_factors, stats, query_users, n_query, a.P, nb_si);
     if (a.n_probe > 0)
         hipLaunchKernelGGL(k_topk_probe,
                            dim3((unsigned)((a.n_probe + kWavesPerBlock - 1) / kWavesPerBlock)),
@@ -1940,14 +2204,26 @@ extern "C" int mf_topk_mm(const int32_t* query_users, int32_t n_query, double gl
         default: MF_MM_LAUNCH(32); break;
     }
 #undef MF_MM_LAUNCH
+    // the users with <= 64 band entries one wave each, then the others one
+    // workgroup each (MF_TOPK_MERGE_WAVE=0: all by workgroups, probes)
+    const char* mwv = std::getenv("MF_TOPK_MERGE_WAVE");
+    const bool wave_merge = !(mwv && mwv[0] == '0');
+    if (!wave_merge) a.big = nullptr;
+    const dim3 grid_mrg((unsigned)((n_query + kWavesPerBlock - 1) / kWavesPerBlock));
+    // the listed users (usually none) by a grid of resident workgroups
+    const dim3 grid_big((unsigned)(wave_merge ? std::min<int32_t>(n_query, 512) : n_query));
+#define MF_MERGE_LAUNCH(GS)                                                                      \
+    if (wave_merge)                                                                           \
+        hipLaunchKernelGGL(k_topk_mm_merge_wave<GS>, grid_mrg, dim3(kBlock), 0, st, a, out_items, \
+                           (float*)out_scores);                                               \
+    hipLaunchKernelGGL(k_topk_mm_merge<GS>, grid_big, dim3(kBlock), 0, st, a, out_items,        \
+                       (float*)out_scores);
     switch (kpad_of(n_factors)) {
-        case 16: hipLaunchKernelGGL(k_topk_mm_merge<16>, dim3((unsigned)n_query), dim3(kBlock), 0,
-                                    st, a, out_items, (float*)out_scores); break;
-        case 32: hipLaunchKernelGGL(k_topk_mm_merge<32>, dim3((unsigned)n_query), dim3(kBlock), 0,
-                                    st, a, out_items, (float*)out_scores); break;
-        default: hipLaunchKernelGGL(k_topk_mm_merge<64>, dim3((unsigned)n_query), dim3(kBlock), 0,
-                                    st, a, out_items, (float*)out_scores); break;
+        case 16: MF_MERGE_LAUNCH(16); break;
+        case 32: MF_MERGE_LAUNCH(32); break;
+        default: MF_MERGE_LAUNCH(64); break;
     }
+#undef MF_MERGE_LAUNCH
     MF_HIP_CHECK(hipGetLastError());
     return MF_OK;
 }

@@ -390,6 +390,35 @@ def test_topk_mfma_filter_ties_and_overflow():
     assert np.array_equal(ids, ei)
 
 
+@pytest.mark.parametrize("merge_wave", ["1", "0"])
+@pytest.mark.parametrize("ties", [False, True])
+def test_topk_merge_forms_agree(ties, merge_wave, monkeypatch):
+    """The merge of the splits' bands -- one wave per user for users whose
+    bands hold <= 64 entries (round 6), one workgroup per user for the rest,
+    or for every user with MF_TOPK_MERGE_WAVE=0 -- gives exactly mf_topk's
+    ids and scores: random scores (small bands, the wave form) and 160
+    exactly tied top items spread over all 8 splits (bands of 160 entries,
+    the workgroup form)."""
+    monkeypatch.setenv("MF_TOPK_MERGE_WAVE", merge_wave)
+    k, nu, ni = 64, 2000, 20000
+    eng = _topk_engine(k, nu, ni, 91)
+    if ties:
+        P, Q, bu, bi = (np.array(x, np.float32) for x in eng.params_numpy())
+        # 20 in each of the 8 item splits (2528 ids each: the split length
+        # rounded up to whole 32-item tiles), within the 32 a list keeps
+        tied = np.array([t * 2528 + 100 + j for t in range(8) for j in range(20)])
+        Q[tied] = Q[tied[0]]
+        bi[tied] = 10.0                   # above every other score of every user
+        eng.load_params(P, Q, bu, bi)
+    users = np.arange(nu, dtype=np.int32)
+    mi, ms, ei, es, fell_back = _topk_both(eng, users, 10)
+    assert not fell_back
+    assert np.array_equal(mi, ei)
+    assert np.array_equal(ms, es)
+    if ties:
+        assert np.array_equal(np.sort(mi, axis=1), np.tile(np.sort(tied)[:10], (nu, 1)))
+
+
 @pytest.mark.parametrize("bf16", ["1", "0"])
 @pytest.mark.parametrize("ni", [20000, 65600])
 def test_topk_probe_floor_with_excluded_top_items(ni, bf16, monkeypatch):
