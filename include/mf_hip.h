@@ -691,6 +691,16 @@ int mf_first_appearance(const int64_t* dense, int64_t base, int64_t n_dense, con
                         int64_t n, int64_t* codes, int64_t* order, int64_t* n_uniques);
 int mf_gather(const void* src, int64_t n_src, int32_t elem_bytes, const int64_t* idx, int64_t n,
               void* dst);
+/* mf_gather with 32-bit indices: the relabelled strata plans' host ids
+ * (user x -> pu[x] over 10^8 int32 ids, engine.py _build_regroup). */
+int mf_gather_i32(const void* src, int64_t n_src, int32_t elem_bytes, const int32_t* idx,
+                  int64_t n, void* dst);
+/* dst[p] = (int32)src[p] for ids in [0, bound) (else MF_ERR_INVALID; bound
+ * <= 2^31), and dst[p] = (float)src[p]: the engine's host ids and FP32
+ * ratings from fit()'s int64 codes and float64 ratings, threaded
+ * (kernel_matrix_factorization.py _make_engine). */
+int mf_ids_to_i32(const int64_t* src, int64_t n, int64_t bound, int32_t* dst);
+int mf_f64_to_f32(const double* src, int64_t n, float* dst);
 /* 64-bit fingerprint of a HOST buffer (threaded, not cryptographic): lets the
  * estimator tell whether the device copy of a parameter array is still the
  * NumPy attribute's content (the reference predicts from the live arrays,

@@ -25,7 +25,10 @@
 //                        of the unshuffled one (computed while the
 //                        permutation is drawn): first shuffled position per
 //                        id by atomic min, ranks by bitmap + prefix popcount.
-//   mf_gather            threaded, prefetched dst[p] = src[idx[p]].
+//   mf_gather            threaded, prefetched dst[p] = src[idx[p]] (64-bit
+//                        indices; mf_gather_i32: 32-bit).
+//   mf_ids_to_i32,       threaded narrowing of the engine's inputs (ids
+//   mf_f64_to_f32        range-checked).
 #include <algorithm>
 #include <climits>
 #include <atomic>
@@ -702,42 +705,97 @@ extern "C" int mf_first_appearance(const int64_t* dense, int64_t base, int64_t n
     return MF_OK;
 }
 
-extern "C" int mf_gather(const void* src, int64_t n_src, int32_t elem_bytes, const int64_t* idx,
-                         int64_t n, void* dst) {
+namespace {
+// dst[p] = src[idx[p]] on the host threads, each source element prefetched a
+// few rows ahead; false when an index falls outside [0, n_src)
+template <typename E, typename I>
+bool gather_rows(const E* s, int64_t n_src, const I* idx, int64_t n, E* d) {
+    std::atomic<int> bad{0};
+    parallel_chunks(n, host_threads(), [&](int, int64_t lo, int64_t hi) {
+        constexpr int kAhead = 16;
+        for (int64_t p = lo; p < hi; ++p) {
+            if (p + kAhead < hi) {
+                const int64_t q = idx[p + kAhead];
+                if (q >= 0 && q < n_src) __builtin_prefetch(s + q, 0, 0);
+            }
+            const int64_t q = idx[p];
+            if (q < 0 || q >= n_src) {
+                bad.store(1);
+                return;
+            }
+            d[p] = s[q];
+        }
+    });
+    return !bad.load();
+}
+
+template <typename I>
+int gather_any(const char* who, const void* src, int64_t n_src, int32_t elem_bytes, const I* idx,
+               int64_t n, void* dst) {
     if (n < 0 || n_src < 0 || (elem_bytes != 4 && elem_bytes != 8) ||
         (n > 0 && (!src || !idx || !dst))) {
-        set_error("mf_gather: bad arguments");
+        set_error("%s: bad arguments", who);
+        return MF_ERR_INVALID;
+    }
+    const bool ok = elem_bytes == 4
+                        ? gather_rows(static_cast<const uint32_t*>(src), n_src, idx, n,
+                                      static_cast<uint32_t*>(dst))
+                        : gather_rows(static_cast<const uint64_t*>(src), n_src, idx, n,
+                                      static_cast<uint64_t*>(dst));
+    if (!ok) {
+        set_error("%s: index outside [0, %lld)", who, (long long)n_src);
+        return MF_ERR_INVALID;
+    }
+    return MF_OK;
+}
+}  // namespace
+
+extern "C" int mf_gather(const void* src, int64_t n_src, int32_t elem_bytes, const int64_t* idx,
+                         int64_t n, void* dst) {
+    return gather_any("mf_gather", src, n_src, elem_bytes, idx, n, dst);
+}
+
+// the same with 32-bit indices (relabelling 10^8 int32 ids through an id
+// permutation: the relabelled plans' host ids)
+extern "C" int mf_gather_i32(const void* src, int64_t n_src, int32_t elem_bytes,
+                             const int32_t* idx, int64_t n, void* dst) {
+    return gather_any("mf_gather_i32", src, n_src, elem_bytes, idx, n, dst);
+}
+
+// fit()'s id columns (int64 codes) narrowed to the engine's int32 ids, each
+// checked against [0, bound), and its ratings narrowed to FP32 -- on the host
+// threads, which also take the destination's first-touch page faults (the
+// NumPy conversions of 10^8 rows ran on one thread on fit()'s critical path)
+extern "C" int mf_ids_to_i32(const int64_t* src, int64_t n, int64_t bound, int32_t* dst) {
+    if (n < 0 || bound < 0 || bound > ((int64_t)1 << 31) || (n > 0 && (!src || !dst))) {
+        set_error("mf_ids_to_i32: bad arguments");
         return MF_ERR_INVALID;
     }
     std::atomic<int> bad{0};
-    auto run = [&](auto tag) {
-        using E = decltype(tag);
-        const E* s = static_cast<const E*>(src);
-        E* d = static_cast<E*>(dst);
-        parallel_chunks(n, host_threads(), [&](int, int64_t lo, int64_t hi) {
-            constexpr int kAhead = 16;
-            for (int64_t p = lo; p < hi; ++p) {
-                if (p + kAhead < hi) {
-                    const int64_t q = idx[p + kAhead];
-                    if (q >= 0 && q < n_src) __builtin_prefetch(s + q, 0, 0);
-                }
-                const int64_t q = idx[p];
-                if (q < 0 || q >= n_src) {
-                    bad.store(1);
-                    return;
-                }
-                d[p] = s[q];
-            }
-        });
-    };
-    if (elem_bytes == 4)
-        run(uint32_t{});
-    else
-        run(uint64_t{});
+    parallel_chunks(n, host_threads(), [&](int, int64_t lo, int64_t hi) {
+        int any = 0;
+        for (int64_t p = lo; p < hi; ++p) {
+            const int64_t v = src[p];
+            any |= (v < 0) | (v >= bound);
+            dst[p] = (int32_t)v;
+        }
+        if (any) bad.store(1);
+    });
     if (bad.load()) {
-        set_error("mf_gather: index outside [0, %lld)", (long long)n_src);
+        set_error("mf_ids_to_i32: an id outside [0, %lld)", (long long)bound);
         return MF_ERR_INVALID;
     }
+    return MF_OK;
+}
+
+extern "C" int mf_f64_to_f32(const double* src, int64_t n, float* dst) {
+    if (n < 0 || (n > 0 && (!src || !dst))) {
+        set_error("mf_f64_to_f32: bad arguments");
+        return MF_ERR_INVALID;
+    }
+    parallel_chunks(n, host_threads(), [&](int, int64_t lo, int64_t hi) {
+        for (int64_t p = lo; p < hi; ++p) dst[p] = (float)src[p];
+    });
     return MF_OK;
 }
 

@@ -137,6 +137,9 @@ SIGNATURES = {
     "mf_id_range": (ctypes.c_int, [_P, _I64, _P, _P]),
     "mf_first_appearance": (ctypes.c_int, [_P, _I64, _I64, _P, _I64, _P, _P, _P]),
     "mf_gather": (ctypes.c_int, [_P, _I64, _I32, _P, _I64, _P]),
+    "mf_gather_i32": (ctypes.c_int, [_P, _I64, _I32, _P, _I64, _P]),
+    "mf_ids_to_i32": (ctypes.c_int, [_P, _I64, _I64, _P]),
+    "mf_f64_to_f32": (ctypes.c_int, [_P, _I64, _P]),
     "mf_fingerprint": (ctypes.c_uint64, [_P, _I64]),
 }
 

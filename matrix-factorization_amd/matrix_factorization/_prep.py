@@ -136,12 +136,31 @@ def factorize_shuffled(dense, perm: np.ndarray):
 
 
 def gather(src: np.ndarray, idx: np.ndarray) -> np.ndarray:
-    """``src[idx]`` for a 1-D array of 4- or 8-byte elements (threaded)."""
+    """``src[idx]`` for a 1-D array of 4- or 8-byte elements (threaded);
+    int32 indices are used as they are (mf_gather_i32), others as int64."""
     src = np.ascontiguousarray(src)
-    idx = np.ascontiguousarray(idx, dtype=np.int64)
+    i32 = isinstance(idx, np.ndarray) and idx.dtype == np.int32
+    idx = np.ascontiguousarray(idx, dtype=np.int32 if i32 else np.int64)
     if src.ndim != 1 or src.dtype.itemsize not in (4, 8) or src.dtype.hasobject:
         return src[idx]
     dst = np.empty(len(idx), src.dtype)
-    _lib.call("mf_gather", _ptr(src), len(src), src.dtype.itemsize, _ptr(idx), len(idx),
-              _ptr(dst))
+    _lib.call("mf_gather_i32" if i32 else "mf_gather", _ptr(src), len(src), src.dtype.itemsize,
+              _ptr(idx), len(idx), _ptr(dst))
     return dst
+
+
+def ids_to_i32(ids: np.ndarray, bound: int) -> np.ndarray:
+    """int64 ids -> int32, each checked against [0, bound) (threaded;
+    MFLibraryError if one is outside)."""
+    ids = np.ascontiguousarray(ids, dtype=np.int64)
+    out = np.empty(len(ids), np.int32)
+    _lib.call("mf_ids_to_i32", _ptr(ids), len(ids), int(bound), _ptr(out))
+    return out
+
+
+def f64_to_f32(x: np.ndarray) -> np.ndarray:
+    """float64 -> float32 (threaded; NumPy's round-to-nearest cast)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    out = np.empty(len(x), np.float32)
+    _lib.call("mf_f64_to_f32", _ptr(x), len(x), _ptr(out))
+    return out

@@ -1012,14 +1012,19 @@ class SGDEngine:
     def _build_regroup(self, j: int, B: int, phases, classes: int, waves):
         """Regrouping j's engine and its device permutations (pu, pi)."""
         rs = np.random.RandomState(self.REGROUP_SEED + j)
-        pu = torch.from_numpy(rs.permutation(self.n_users).astype(np.int64)).to(self.dev)
-        pi = torch.from_numpy(rs.permutation(self.n_items).astype(np.int64)).to(self.dev)
-        uj_d = pu.index_select(0, self.u.long()).to(torch.int32)
-        ij_d = pi.index_select(0, self.i.long()).to(torch.int32)
-        # the relabelled ids stay on the device for the engine (no re-upload),
-        # the ratings are this engine's (read-only); the host copies feed the
-        # planner
-        e = SGDEngine(uj_d.cpu().numpy(), ij_d.cpu().numpy(), self.r_host, self.n_users,
+        pu_h = rs.permutation(self.n_users).astype(np.int32)
+        pi_h = rs.permutation(self.n_items).astype(np.int32)
+        pu = torch.from_numpy(pu_h).to(self.dev)
+        pi = torch.from_numpy(pi_h).to(self.dev)
+        uj_d = pu.index_select(0, self.u)
+        ij_d = pi.index_select(0, self.i)
+        # the relabelled ids: on the device for the engine (no upload), and
+        # relabelled on the host threads for the planner (no read-back of
+        # 2 x 4 bytes per rating); the ratings are this engine's (read-only)
+        uj_h = _prep.gather(pu_h, self.u_host)
+        ij_h = _prep.gather(pi_h, self.i_host)
+        pu, pi = pu.long(), pi.long()
+        e = SGDEngine(uj_h, ij_h, self.r_host, self.n_users,
                       self.n_items, self.k, self.kernel, self.dtype, self.dev, self.gamma,
                       self.min_rating, self.max_rating, self.global_mean, eval_order=False,
                       check_ids=False, device_triples=(uj_d, ij_d, self.r))

@@ -68,10 +68,13 @@ from typing import Union
 import numpy as np
 import pandas as pd
 
-from . import _lib
+from . import _lib, _prep
 from .distributed import EXCHANGES, fit_sharded, world_info
 from .engine import SGDEngine, canonical_dtype, fit_epochs, resolve_device
 from .recommender_base import RecommenderBase
+
+# fit() inputs from this many rows are narrowed natively (_make_engine)
+NATIVE_NARROW_MIN_ROWS = 1 << 20
 
 
 def _fingerprint(a) -> tuple:
@@ -172,15 +175,30 @@ class KernelMF(RecommenderBase):
 
         dev = resolve_device(self.device) if device is None else device
         n = len(X)
-        u = X["user_id"].to_numpy(np.int32) if n else np.zeros(0, np.int32)
-        i = X["item_id"].to_numpy(np.int32) if n else np.zeros(0, np.int32)
+        cu, ci = X["user_id"], X["item_id"]
+        checked = False
+        if n >= NATIVE_NARROW_MIN_ROWS and cu.dtype == np.int64 and ci.dtype == np.int64:
+            # 10^8-row columns narrowed (and range-checked) on the host
+            # threads rather than by NumPy's one-thread casts
+            try:
+                u = _prep.ids_to_i32(cu.to_numpy(), n_users)
+                i = _prep.ids_to_i32(ci.to_numpy(), n_items)
+            except _lib.MFLibraryError:
+                raise ValueError("rating ids outside [0, n_users) x [0, n_items)") from None
+            checked = True
+        else:
+            u = cu.to_numpy(np.int32) if n else np.zeros(0, np.int32)
+            i = ci.to_numpy(np.int32) if n else np.zeros(0, np.int32)
         r = X["rating"].to_numpy(np.float64) if n else np.zeros(0)
+        if n >= NATIVE_NARROW_MIN_ROWS and canonical_dtype(self.dtype) == "float32":
+            r = _prep.f64_to_f32(r)
         on_gpu = isinstance(dev, torch.device) and dev.type == "cuda"
         with (torch.cuda.device(dev) if on_gpu else contextlib.nullcontext()):
             eng = SGDEngine(u, i, r, n_users, n_items,
                             self.n_factors, self.kernel, self.dtype, dev,
                             gamma=self.gamma, min_rating=self.min_rating,
-                            max_rating=self.max_rating, global_mean=self.global_mean)
+                            max_rating=self.max_rating, global_mean=self.global_mean,
+                            **({"check_ids": False} if checked else {}))
             eng.strata_classes = getattr(self, "strata_classes", "auto")
             eng.strata_regroup = getattr(self, "strata_regroup", "auto")
             if schedule == "strata" and n:

@@ -166,14 +166,39 @@ def test_pairs_duplicated_is_pandas(n):
     assert not _prep.pairs_duplicated(np.array([1, 2]), np.array([2, 1]))
 
 
-def test_gather_and_bounds():
+@pytest.mark.parametrize("idx_dtype", [np.int64, np.int32])
+def test_gather_and_bounds(idx_dtype):
+    """mf_gather (int64 indices) and mf_gather_i32 (int32 indices: the
+    relabelled plans' host ids): src[idx], out-of-range indices refused."""
     rs = np.random.RandomState(0)
     for dt in (np.float32, np.float64, np.int32, np.int64):
         src = rs.randint(0, 1000, 100_000).astype(dt)
-        idx = rs.randint(0, len(src), 250_000)
+        idx = rs.randint(0, len(src), 250_000).astype(idx_dtype)
         assert np.array_equal(_prep.gather(src, idx), src[idx])
+    for bad in ([0, 10], [-1, 0]):
+        with pytest.raises(_lib.MFLibraryError):
+            _prep.gather(np.zeros(10, np.float32), np.array(bad, idx_dtype))
+
+
+def test_native_narrowing_is_numpys():
+    """The engine's inputs narrowed on the host threads (_make_engine at
+    10^8 rows): int64 ids -> int32 with the [0, bound) check, float64
+    ratings -> float32 as NumPy casts them (NaN, inf, overflow included)."""
+    rs = np.random.RandomState(4)
+    ids = rs.randint(0, 70_000, 2_000_003).astype(np.int64)
+    assert np.array_equal(_prep.ids_to_i32(ids, 70_000), ids.astype(np.int32))
+    for bad in (69_999, ):
+        with pytest.raises(_lib.MFLibraryError):
+            _prep.ids_to_i32(ids, bad)
+    neg = ids.copy()
+    neg[1_234_567] = -1
     with pytest.raises(_lib.MFLibraryError):
-        _prep.gather(np.zeros(10, np.float32), np.array([0, 10]))
+        _prep.ids_to_i32(neg, 70_000)
+    x = rs.normal(0, 1e3, 2_000_001)
+    x[[3, 4, 5, 6]] = [np.nan, np.inf, -1e300, 3.4028235677973366e38]
+    with np.errstate(over="ignore"):
+        want = x.astype(np.float32)
+    assert np.array_equal(_prep.f64_to_f32(x), want, equal_nan=True)
 
 
 def _frame(n, dtype, seed, index=None):
