@@ -683,6 +683,23 @@ int mf_legacy_shuffle(uint32_t* mt_key, int32_t* mt_pos, int64_t* data, int64_t 
  * runs on 32-bit rating indices. */
 int mf_legacy_shuffle_i32(uint32_t* mt_key, int32_t* mt_pos, int32_t* data, int64_t n);
 int mf_legacy_permutation(uint32_t* mt_key, int32_t* mt_pos, int64_t* out, int64_t n);
+/* np.random.shuffle of n elements in two parts (the exact schedule's
+ * per-epoch shuffle, kernel_matrix_factorization.py:371, with its swaps on the
+ * GPU): mf_legacy_shuffle_draws makes the draws only -- targets[d] = the
+ * position swapped with n-1-d, d = 0 .. n-2 -- advancing the MT19937 state
+ * exactly as the whole shuffle does; mf_legacy_apply_swaps_i32 applies swaps
+ * d_begin .. n-2 of them, in order, on the host; mf_shuffle_swaps_device
+ * (device pointers; stream a hipStream_t) applies swaps 0 .. d_end-1 on the
+ * GPU by rounds of deterministic reservations (the same result as in
+ * order): reservations = n zeroed 64-bit words kept between calls, tag_io =
+ * the next round tag (start at 1; advanced), workspace >=
+ * mf_shuffle_swaps_workspace_bytes(n). */
+int mf_legacy_shuffle_draws(uint32_t* mt_key, int32_t* mt_pos, int64_t n, uint32_t* targets);
+int mf_legacy_apply_swaps_i32(const uint32_t* targets, int64_t n, int64_t d_begin, int32_t* data);
+size_t mf_shuffle_swaps_workspace_bytes(int64_t n);
+int mf_shuffle_swaps_device(const uint32_t* targets, int64_t n, int64_t d_end, int32_t* data,
+                            unsigned long long* reservations, void* workspace, uint64_t* tag_io,
+                            void* stream);
 int mf_pairs_duplicated(const int64_t* a, const int64_t* b, int64_t n, int32_t* has_dup);
 int mf_factorize(const int64_t* vals, int64_t n, int64_t* codes, int64_t* uniques,
                  int64_t* n_uniques);

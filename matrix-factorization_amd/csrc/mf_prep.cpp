@@ -359,6 +359,37 @@ void shuffle_any(MT& mt, E* data, int64_t n) {
         shuffle_raw(mt, data, n);
 }
 
+// the draws of shuffle_raw alone: the swap targets j_d (d = 0 .. total-1,
+// swap d exchanging x[total - d] and x[j_d]) into tgt
+void draw_targets(MT& mt, uint32_t* tgt, int64_t total) {
+    const bool simd = use_avx512();
+    int64_t R = 1;
+    while (R < total + 16) R <<= 1;                 // tgt is indexed by d itself
+    int64_t d = 0;
+    uint32_t maxv = (uint32_t)total;
+    while (d < total) {
+        int p;
+        if (simd) {
+            if (mt.pos == kN) mt_regen_512(mt);
+            p = mt.pos;
+            mt_draws_512(mt, p, d, maxv, total, tgt, R, (int32_t*)nullptr, false);
+        } else {
+            if (mt.pos == kN) mt.regen();
+            p = mt.pos;
+            while (p < kN) {
+                const uint32_t mask = 0xffffffffu >> __builtin_clz(maxv);
+                const uint32_t v = mt_temper(mt.key[p++]) & mask;
+                const uint32_t acc = v <= maxv ? 1u : 0u;
+                tgt[d] = v;
+                d += acc;
+                maxv -= acc;
+                if (d == total) break;
+            }
+        }
+        mt.pos = p;
+    }
+}
+
 int load_mt(MT& mt, const uint32_t* mt_key, const int32_t* mt_pos, int64_t n, const char* who) {
     if (n - 1 > (int64_t)0xffffffffLL) {
         set_error("%s: n = %lld exceeds the 32-bit draw range", who, (long long)n);
@@ -385,6 +416,49 @@ extern "C" int mf_legacy_shuffle(uint32_t* mt_key, int32_t* mt_pos, int64_t* dat
     shuffle_any(mt, data, n);
     std::memcpy(mt_key, mt.key, sizeof(mt.key));
     *mt_pos = mt.pos;
+    return MF_OK;
+}
+
+// The shuffle in two parts (the exact schedule's shuffle on the GPU,
+// engine.ExactShuffler): the draws here, on one thread -- the RandomState
+// advanced exactly as by the whole shuffle -- and the swaps wherever they
+// are applied (mf_shuffle_swaps_device; mf_legacy_apply_swaps_i32 for the
+// last ones, on the host).
+extern "C" int mf_legacy_shuffle_draws(uint32_t* mt_key, int32_t* mt_pos, int64_t n,
+                                       uint32_t* targets) {
+    if (!mt_key || !mt_pos || n < 0 || (n > 1 && !targets)) {
+        set_error("mf_legacy_shuffle_draws: null pointer or negative n");
+        return MF_ERR_INVALID;
+    }
+    MT mt;
+    if (const int rc = load_mt(mt, mt_key, mt_pos, n, "mf_legacy_shuffle_draws")) return rc;
+    if (n > 1) draw_targets(mt, targets, n - 1);
+    std::memcpy(mt_key, mt.key, sizeof(mt.key));
+    *mt_pos = mt.pos;
+    return MF_OK;
+}
+
+// swaps d = d_begin .. n-2 of the shuffle of data[0 .. n) whose draws are
+// `targets` (swap d: data[n-1-d] <-> data[targets[d]]), in order
+extern "C" int mf_legacy_apply_swaps_i32(const uint32_t* targets, int64_t n, int64_t d_begin,
+                                         int32_t* data) {
+    const int64_t total = n - 1;
+    if (n < 0 || d_begin < 0 || (n > 1 && d_begin < total && (!targets || !data))) {
+        set_error("mf_legacy_apply_swaps_i32: bad arguments");
+        return MF_ERR_INVALID;
+    }
+    for (int64_t d = d_begin; d < total; ++d) {
+        if (d + 32 < total) __builtin_prefetch(data + targets[d + 32], 1, 1);
+        const int64_t i = total - d, j = targets[d];
+        if (j > i) {
+            set_error("mf_legacy_apply_swaps_i32: target %lld of swap %lld past %lld",
+                      (long long)j, (long long)d, (long long)i);
+            return MF_ERR_INVALID;
+        }
+        const int32_t x = data[i];
+        data[i] = data[j];
+        data[j] = x;
+    }
     return MF_OK;
 }
 

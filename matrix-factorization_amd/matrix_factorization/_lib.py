@@ -132,6 +132,10 @@ SIGNATURES = {
     "mf_legacy_shuffle": (ctypes.c_int, [_P, _P, _P, _I64]),
     "mf_legacy_shuffle_i32": (ctypes.c_int, [_P, _P, _P, _I64]),
     "mf_legacy_permutation": (ctypes.c_int, [_P, _P, _P, _I64]),
+    "mf_legacy_shuffle_draws": (ctypes.c_int, [_P, _P, _I64, _P]),
+    "mf_legacy_apply_swaps_i32": (ctypes.c_int, [_P, _I64, _I64, _P]),
+    "mf_shuffle_swaps_workspace_bytes": (ctypes.c_size_t, [_I64]),
+    "mf_shuffle_swaps_device": (ctypes.c_int, [_P, _I64, _I64, _P, _P, _P, _P, _P]),
     "mf_pairs_duplicated": (ctypes.c_int, [_P, _P, _I64, _P]),
     "mf_factorize": (ctypes.c_int, [_P, _I64, _P, _P, _P]),
     "mf_id_range": (ctypes.c_int, [_P, _I64, _P, _P]),

@@ -61,6 +61,32 @@ def legacy_permutation(n: int) -> np.ndarray:
     return perm
 
 
+def legacy_shuffle_draws(n: int, targets: np.ndarray) -> None:
+    """The draws of ``np.random.shuffle`` of n elements, without the swaps:
+    ``targets[d]`` (uint32 bits, d = 0 .. n-2) = the position swapped with
+    n-1-d; the global RandomState is advanced exactly as by the shuffle."""
+    st = np.random.get_state()
+    if st[0] != "MT19937" or n > _MAX_N:         # pragma: no cover - legacy is MT19937
+        raise ValueError("legacy_shuffle_draws: MT19937 and n <= 2^32 + 1 only")
+    if n > 1 and (targets.dtype.itemsize != 4 or not targets.flags.c_contiguous
+                  or len(targets) < n - 1):
+        raise ValueError("targets must be a contiguous 4-byte array of n - 1 entries")
+    key = np.ascontiguousarray(st[1], dtype=np.uint32).copy()
+    pos = ctypes.c_int32(int(st[2]))
+    _lib.call("mf_legacy_shuffle_draws", _ptr(key), ctypes.addressof(pos), n,
+              _ptr(targets) if n > 1 else None)
+    np.random.set_state(("MT19937", key, pos.value, st[3], st[4]))
+
+
+def apply_swaps_i32(targets: np.ndarray, n: int, d_begin: int, data: np.ndarray) -> None:
+    """Swaps d_begin .. n-2 of a shuffle drawn by legacy_shuffle_draws,
+    applied in order to the int32 array ``data`` of n elements."""
+    if data.dtype != np.int32 or not data.flags.c_contiguous or len(data) < n:
+        raise ValueError("data must be a contiguous int32 array of n entries")
+    _lib.call("mf_legacy_apply_swaps_i32", _ptr(targets) if n > 1 else None, n, d_begin,
+              _ptr(data))
+
+
 def as_int64_ids(col: np.ndarray):
     """The id column as int64 (a view or a widening copy) when its values can
     be hashed as 64-bit integers with equality preserved, else None."""

@@ -1939,6 +1939,91 @@ class _ErrorPoll:
 
 # the exact schedule pipelines its per-epoch shuffle from this many ratings
 EXACT_PIPELINE_MIN = 1 << 20
+# ... and applies the shuffle's swaps on the GPU from this many
+EXACT_GPU_SHUFFLE_MIN = 1 << 22
+
+
+class ExactShuffler:
+    """``np.random.shuffle`` of the exact schedule's 32-bit visit order (the
+    reference's per-epoch shuffle, kernel_matrix_factorization.py:371) with
+    the draws on the calling thread (mf_legacy_shuffle_draws: the RandomState
+    advanced as by the shuffle) and the swaps on the GPU
+    (mf_shuffle_swaps_device, rounds of deterministic reservations) on a
+    stream of its own, except the last ones (positions below TAIL), applied
+    on the host after the read-back -- the same order as NumPy's, bit for bit.
+    One host thread made the whole shuffle the exact epoch's bound at C3
+    (0.24 s).  The device keeps the order it produced,
+    so a call on the previous call's result uploads nothing; the result
+    arrays are two pinned buffers used in turn (a result stays valid until
+    the second call after it)."""
+
+    TAIL = 1 << 20
+
+    def __init__(self, n: int, dev):
+        lib = _lib.load()
+        self.n, self.dev = int(n), dev
+        self.total = max(self.n - 1, 0)
+        # swaps d < d_end have i = total - d >= TAIL; the rest touch [0, TAIL)
+        self.d_end = max(0, self.total - self.TAIL + 1)
+        m = max(self.total, 1)
+        with torch.cuda.device(dev):
+            self.tgt_h = torch.empty(m, dtype=torch.int32, pin_memory=True)
+            self.tgt_d = torch.empty(m, dtype=torch.int32, device=dev)
+            self.res = torch.zeros(max(self.n, 1), dtype=torch.int64, device=dev)
+            wsb = int(lib.mf_shuffle_swaps_workspace_bytes(self.n))
+            self.ws = torch.empty((wsb + 7) // 8, dtype=torch.int64, device=dev)
+            self.ord_d = [torch.empty(max(self.n, 1), dtype=torch.int32, device=dev)
+                          for _ in range(2)]
+            self.ord_h = [torch.empty(max(self.n, 1), dtype=torch.int32, pin_memory=True)
+                          for _ in range(2)]
+            self.stream = torch.cuda.Stream(dev)
+        self.tag = ctypes.c_uint64(1)
+        self.cur = None                  # ord_d / ord_h index of the last result
+        self.last = None                 # ... that result (the host array returned)
+
+    def shuffle_from(self, src: np.ndarray) -> np.ndarray:
+        """shuffle(copy of src): a new array, src untouched."""
+        n = self.n
+        if len(src) != n or src.dtype != np.int32:
+            raise ValueError("src must hold n int32 entries")
+        o = 0 if self.cur != 0 else 1
+        tgt = self.tgt_h.numpy().view(np.uint32)
+        _prep.legacy_shuffle_draws(n, tgt)
+        dst_h = self.ord_h[o].numpy()[:n]
+        with torch.cuda.device(self.dev), torch.cuda.stream(self.stream):
+            if self.cur is not None and src is self.last:
+                base = self.ord_d[self.cur]
+            else:                        # an order this shuffler did not make
+                base = self.ord_d[o]
+                base[:n].copy_(torch.from_numpy(src), non_blocking=False)
+            dst = self.ord_d[o]
+            if base is not dst:
+                dst[:n].copy_(base[:n])
+            if self.d_end > 0:
+                self.tgt_d[: self.total].copy_(self.tgt_h[: self.total], non_blocking=True)
+                _lib.call("mf_shuffle_swaps_device", _tp(self.tgt_d), n, self.d_end, _tp(dst),
+                          _tp(self.res), _tp(self.ws), ctypes.byref(self.tag),
+                          _VOID(self.stream.cuda_stream))
+            self.ord_h[o][:n].copy_(dst[:n], non_blocking=True)
+            self.stream.synchronize()
+            _prep.apply_swaps_i32(tgt, n, self.d_end, dst_h)
+            if self.d_end > 0:           # the host's swaps back to the device copy
+                t = min(self.TAIL, n)
+                dst[:t].copy_(self.ord_h[o][:t], non_blocking=True)
+        self.cur, self.last = o, dst_h
+        return dst_h
+
+
+def exact_shuffler(engine: "SGDEngine"):
+    """The engine's ExactShuffler when its ratings are many enough and it is
+    on a GPU (env MF_EXACT_GPU_SHUFFLE=0: none, the host shuffle)."""
+    if (engine.n < EXACT_GPU_SHUFFLE_MIN or engine.dev.type != "cuda"
+            or os.environ.get("MF_EXACT_GPU_SHUFFLE") == "0"):
+        return None
+    sh = getattr(engine, "_exact_shuffler", None)
+    if sh is None or sh.n != engine.n:
+        sh = engine._exact_shuffler = ExactShuffler(engine.n, engine.dev)
+    return sh
 
 
 def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
@@ -1983,8 +2068,11 @@ def fit_epochs(engine: SGDEngine, n_epochs: int, schedule: str, lr: float,
         if pipeline:
             exact_pool = ThreadPoolExecutor(1)
             exact_spare = np.empty_like(order)
+            shuffler = exact_shuffler(engine)
 
             def shuffled_copy(src, dst):
+                if shuffler is not None:          # the swaps on the GPU
+                    return shuffler.shuffle_from(src)
                 # (torch's CPU copy is threaded: 400 MB at C3 in ~10 ms
                 # instead of np.copyto's ~40 ms on the worker's critical path)
                 torch.from_numpy(dst).copy_(torch.from_numpy(src))
