@@ -80,9 +80,10 @@ def legacy_shuffle_draws(n: int, targets: np.ndarray) -> None:
 
 def apply_swaps_i32(targets: np.ndarray, n: int, d_begin: int, data: np.ndarray) -> None:
     """Swaps d_begin .. n-2 of a shuffle drawn by legacy_shuffle_draws,
-    applied in order to the int32 array ``data`` of n elements."""
-    if data.dtype != np.int32 or not data.flags.c_contiguous or len(data) < n:
-        raise ValueError("data must be a contiguous int32 array of n entries")
+    applied in order to the int32 array ``data`` -- the first n - d_begin
+    elements of the shuffled array, all those swaps touch."""
+    if data.dtype != np.int32 or not data.flags.c_contiguous or len(data) < n - d_begin:
+        raise ValueError("data must be a contiguous int32 array of n - d_begin entries")
     _lib.call("mf_legacy_apply_swaps_i32", _ptr(targets) if n > 1 else None, n, d_begin,
               _ptr(data))
 

@@ -70,7 +70,8 @@ import pandas as pd
 
 from . import _lib, _prep
 from .distributed import EXCHANGES, fit_sharded, world_info
-from .engine import SGDEngine, canonical_dtype, fit_epochs, resolve_device
+from .engine import (EXACT_GPU_SHUFFLE_MIN, SGDEngine, canonical_dtype, fit_epochs,
+                     legacy_permutation_device, resolve_device)
 from .recommender_base import RecommenderBase
 
 # fit() inputs from this many rows are narrowed natively (_make_engine)
@@ -208,6 +209,19 @@ class KernelMF(RecommenderBase):
             if worker and on_gpu:
                 torch.cuda.current_stream(dev).synchronize()
         return eng
+
+    def _draw_permutation(self, n: int) -> np.ndarray:
+        """X.sample(frac=1)'s draw: at 10^8 rows with the shuffle's swaps on
+        the GPU (legacy_permutation_device; MF_PREP_GPU_PERM=0: the host),
+        the same permutation and RandomState."""
+        import os
+
+        import torch
+
+        if (n >= EXACT_GPU_SHUFFLE_MIN and n < (1 << 31)
+                and os.environ.get("MF_PREP_GPU_PERM") != "0" and torch.cuda.is_available()):
+            return legacy_permutation_device(n, resolve_device(self.device))
+        return super()._draw_permutation(n)
 
     def _sync_params(self, eng: SGDEngine) -> None:
         P, Q, bu, bi = eng.params_numpy()

@@ -117,7 +117,8 @@ class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
         if type in ("fit", "update"):
             ids = self._int64_ids(X)
             if ids is not None:
-                perm, dense = self._checked_permutation(ids, dense=type == "fit")
+                perm, dense = self._checked_permutation(ids, dense=type == "fit",
+                                                        draw=self._draw_permutation)
                 rating = _aligned_rating(X, y) if type == "fit" else None
                 if rating is not None:
                     return self._fit_maps_native(X.index, ids, rating, perm, dense)
@@ -189,8 +190,12 @@ class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
         self._id_dtypes = (cu.dtype, ci.dtype)
         return None if u is None or i is None else (u, i)
 
+    def _draw_permutation(self, n: int) -> np.ndarray:
+        """``np.random.permutation(n)``: X.sample(frac=1)'s draw (int64)."""
+        return _prep.legacy_permutation(n)
+
     @staticmethod
-    def _checked_permutation(ids, dense: bool = False):
+    def _checked_permutation(ids, dense: bool = False, draw=None):
         """(perm, dense ids or None): the duplicate-pair check
         (recommender_base.py:125-128) -- and with ``dense`` the columns'
         ``_prep.dense_ids`` -- on worker threads beside ``X.sample(frac=1)``'s
@@ -200,7 +205,8 @@ class RecommenderBase(BaseEstimator, RegressorMixin, metaclass=ABCMeta):
         with ThreadPoolExecutor(3 if dense else 1) as ex:
             dup = ex.submit(_prep.pairs_duplicated, *ids)
             dn = [ex.submit(_prep.dense_ids, v) for v in ids] if dense else None
-            perm = _prep.legacy_permutation(len(ids[0]))       # = X.sample's draw
+            n = len(ids[0])
+            perm = draw(n) if draw is not None else _prep.legacy_permutation(n)   # = X.sample's
             if dup.result():
                 np.random.set_state(state)
                 raise ValueError("Duplicate user-item ratings in matrix")

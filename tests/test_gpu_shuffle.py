@@ -74,3 +74,21 @@ def test_exact_fit_gpu_swaps_equal_host_shuffle(monkeypatch):
         assert np.array_equal(a, b)
     assert ra == rb
     assert np.array_equal(xa, xb)
+
+
+def test_device_permutation_is_numpys():
+    """fit()'s X.sample(frac=1) draw at 10^8 rows (legacy_permutation_device:
+    the swaps on the GPU): np.random.permutation's result and RandomState."""
+    import torch
+
+    from matrix_factorization.engine import legacy_permutation_device
+
+    n = 5_000_011
+    np.random.seed(8)
+    want = np.random.permutation(n)
+    x_ref = np.random.rand(2)
+    np.random.seed(8)
+    got = legacy_permutation_device(n, torch.device("cuda:0"))
+    assert got.dtype == np.int64
+    assert np.array_equal(got, want)
+    assert np.array_equal(np.random.rand(2), x_ref)
