@@ -2000,6 +2000,9 @@ class ExactShuffler:
             if base is not dst:
                 dst[:n].copy_(base[:n])
             if self.d_end > 0:
+                if self.tag.value > (1 << 30):   # the tags' room: start over
+                    self.res.zero_()
+                    self.tag.value = 1
                 self.tgt_d[: self.total].copy_(self.tgt_h[: self.total], non_blocking=True)
                 _lib.call("mf_shuffle_swaps_device", _tp(self.tgt_d), n, self.d_end, _tp(dst),
                           _tp(self.res), _tp(self.ws), ctypes.byref(self.tag),

@@ -10,9 +10,17 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n", [5_000_003, 4_194_305])
-def test_gpu_shuffle_is_numpys(n):
+@pytest.mark.parametrize("n,rounds", [(5_000_003, None), (4_194_305, None), (4_500_007, "1"),
+                                      (4_500_007, "2")])
+def test_gpu_shuffle_is_numpys(n, rounds, monkeypatch):
+    """Also with one or two reservation rounds (MF_SHUFFLE_GPU_ROUNDS), so
+    that the in-order one-thread fixup takes thousands of stragglers."""
     import torch
+
+    if rounds is None:
+        monkeypatch.delenv("MF_SHUFFLE_GPU_ROUNDS", raising=False)
+    else:
+        monkeypatch.setenv("MF_SHUFFLE_GPU_ROUNDS", rounds)
 
     from matrix_factorization.engine import ExactShuffler
 
