@@ -54,7 +54,7 @@ std::atomic<int64_t> g_phase_ns[4];
 std::atomic<int64_t> g_paths{0}, g_path_len{0};
 
 struct Scratch {
-    std::vector<uint64_t> smask, imask, lvl;
+    std::vector<uint64_t> smask, imask, lvl, ubits;
     std::vector<int32_t> dstart, order;
     std::vector<int32_t> ucnt, uslot, users, load;
     std::vector<int32_t> es, eq, ecol, icnt;
@@ -93,11 +93,14 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, int32_t m,
         S.ucnt.resize(nus, 0);
         S.uslot.resize(nus, -1);
     }
+    const int32_t NW = (nus + 63) >> 6;
+    if ((int32_t)S.ubits.size() < NW) S.ubits.resize(NW, 0);
     S.users.clear();
     int32_t maxdeg = 0;
     for (int32_t x = 0; x < m; ++x) {
         const int32_t ul = bu[x] - ulo;
         if (S.ucnt[ul]++ == 0) S.users.push_back(ul);
+        S.ubits[ul >> 6] |= 1ull << (ul & 63);
         maxdeg = std::max(maxdeg, S.ucnt[ul]);
     }
     // longest processing time first: users by falling degree, ties by id --
@@ -109,10 +112,17 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, int32_t m,
     if ((int64_t)S.users.size() * 8 < nus) {                       // few users: sort them
         std::sort(S.users.begin(), S.users.end());                // ids ascending
         for (int32_t ul : S.users) S.order[(size_t)S.dstart[maxdeg - S.ucnt[ul]]++] = ul;
-    } else {                                                      // else scan the id range
-        for (int32_t ul = 0; ul < nus; ++ul)
-            if (S.ucnt[ul] > 0) S.order[(size_t)S.dstart[maxdeg - S.ucnt[ul]]++] = ul;
+    } else {                        // else the set bits of the id range, ascending
+        for (int32_t w = 0; w < NW; ++w)
+            for (uint64_t b = S.ubits[w]; b; b &= b - 1) {
+                const int32_t ul = w * 64 + __builtin_ctzll(b);
+                S.order[(size_t)S.dstart[maxdeg - S.ucnt[ul]]++] = ul;
+            }
     }
+    if ((int64_t)S.users.size() * 4 < NW)
+        for (int32_t ul : S.users) S.ubits[ul >> 6] = 0;
+    else
+        std::fill(S.ubits.begin(), S.ubits.begin() + NW, 0);
     c1 = clk::now();
     // each user onto the least loaded slot, ties to the lowest slot index
     // (the order a (load, slot) min-heap pops): one bit set of slots per load
