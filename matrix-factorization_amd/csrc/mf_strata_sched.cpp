@@ -53,6 +53,8 @@ namespace {
 std::atomic<int64_t> g_phase_ns[4];
 std::atomic<int64_t> g_paths{0}, g_path_len{0};
 
+struct Trip { int32_t row, u, i; };               // a rating's row and ids
+
 struct Scratch {
     std::vector<uint64_t> smask, imask, lvl, ubits;
     std::vector<int32_t> dstart, order;
@@ -61,14 +63,14 @@ struct Scratch {
     std::vector<int32_t> sc, ic, path;
 };
 
-// Plan one block: its m ratings (user ids bu[], item ids bi[], in row order)
+// Plan one block: its m ratings (bt[]: row, user id, item id; in row order)
 // with item ids in [ilo, ilo+nqi) and user ids in [ulo, ulo+nus).  Returns D
 // and, with `pos`, writes each rating's position in the block's D*NS grid
 // (step * NS + slot) to pos[] (without: the step count only -- D is known
 // before the colouring).  es_save: each rating's slot is written there;
 // es_load: the slots are taken from there (a step-count pass of the same NS)
 // instead of being assigned again.
-int32_t plan_block(const int32_t* bu, const int32_t* bi, int32_t m,
+int32_t plan_block(const Trip* bt, int32_t m,
                    int32_t ilo, int32_t nqi, int32_t ulo, int32_t nus, int32_t NS, Scratch& S,
                    int32_t* pos, int32_t* es_save = nullptr, const int32_t* es_load = nullptr) {
     if (m == 0) return 0;
@@ -82,7 +84,7 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, int32_t m,
         S.icnt.assign(nqi, 0);
         S.load.assign(NS, 0);
         for (int32_t x = 0; x < m; ++x) {
-            S.eq[x] = bi[x] - ilo;
+            S.eq[x] = bt[x].i - ilo;
             D = std::max(D, ++S.icnt[S.eq[x]]);
             D = std::max(D, ++S.load[S.es[x]]);
         }
@@ -98,7 +100,7 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, int32_t m,
     S.users.clear();
     int32_t maxdeg = 0;
     for (int32_t x = 0; x < m; ++x) {
-        const int32_t ul = bu[x] - ulo;
+        const int32_t ul = bt[x].u - ulo;
         if (S.ucnt[ul]++ == 0) S.users.push_back(ul);
         S.ubits[ul >> 6] |= 1ull << (ul & 63);
         maxdeg = std::max(maxdeg, S.ucnt[ul]);
@@ -163,8 +165,8 @@ int32_t plan_block(const int32_t* bu, const int32_t* bi, int32_t m,
     S.es.resize(m);
     S.eq.resize(m);
     for (int32_t x = 0; x < m; ++x) {
-        S.es[x] = S.uslot[bu[x] - ulo];
-        S.eq[x] = bi[x] - ilo;
+        S.es[x] = S.uslot[bt[x].u - ulo];
+        S.eq[x] = bt[x].i - ilo;
         D = std::max(D, ++S.icnt[S.eq[x]]);
     }
     for (int32_t ul : S.users) {
@@ -392,7 +394,6 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
     }
     lap("stratum keys");
     std::vector<int64_t> soff, boff((size_t)BB + 1, 0);
-    struct Trip { int32_t row, u, i; };           // one write stream per bucket
     auto strip = mf::big_alloc<Trip>(n);
     if (!strip) throw std::bad_alloc();
     mf::partition_rows(
@@ -400,7 +401,8 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
         soff, [&](int64_t d, int64_t j) { strip[d] = Trip{(int32_t)j, user_ids[j], item_ids[j]}; });
     key.reset();
     lap("validate + stratum pass");
-    auto b_row = buf(n), b_u = buf(n), b_i = buf(n);
+    auto b_t = mf::big_alloc<Trip>(n);         // one write stream per bucket
+    if (!b_t) throw std::bad_alloc();
     mf::for_buckets(CB, T, [&](int sv) {
         const int64_t lo = soff[sv], hi = soff[sv + 1];
         std::vector<int64_t> cnt((size_t)B + 1, 0);
@@ -410,9 +412,7 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
         for (int64_t d = lo; d < hi; ++d) {
             const Trip t = strip[d];
             const int64_t o = lo + cnt[ib_of[t.i]]++;
-            b_row[o] = t.row;
-            b_u[o] = t.u;
-            b_i[o] = t.i;
+            b_t[o] = t;
         }
     });
     boff[BB] = n;
@@ -447,7 +447,7 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
                     const int32_t ub = (int32_t)(((int64_t)sv + (int64_t)C * w) % CB);
                     const int64_t o = boff[b];
                     steps[b] = plan_block(
-                        b_u.get() + o, b_i.get() + o, (int32_t)(boff[b + 1] - o),
+                        b_t.get() + o, (int32_t)(boff[b + 1] - o),
                         item_bounds[w], item_bounds[w + 1] - item_bounds[w], user_bounds[ub],
                         user_bounds[ub + 1] - user_bounds[ub], NS, S, pos ? pos + o : nullptr,
                         es_save ? es_save + o : nullptr, es_load ? es_load + o : nullptr);
@@ -488,8 +488,6 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
     es_cur.reset();
     blocks(n_slots, b_pos.get(), nullptr, es_best ? es_best.get() : nullptr);
     es_best.reset();
-    b_u.reset();
-    b_i.reset();
     lap("plan blocks");
 
     auto* plan = new (std::nothrow) mf_strata_plan;
@@ -515,7 +513,7 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
         for (int64_t b = c * CH; b < std::min(BB, (c + 1) * CH); ++b) {
             int32_t* grid = sched + plan->bstep[b] * n_slots;
             std::fill(grid, grid + (int64_t)steps[b] * n_slots, -1);
-            for (int64_t e = boff[b]; e < boff[b + 1]; ++e) grid[b_pos[e]] = b_row[e];
+            for (int64_t e = boff[b]; e < boff[b + 1]; ++e) grid[b_pos[e]] = b_t[e].row;
         }
     });
     lap("grids");
