@@ -138,6 +138,48 @@ int32_t plan_block(const Trip* bt, int32_t m,
     for (int32_t x = 0; x < NS; ++x) S.lvl[(size_t)(x >> 6)] |= 1ull << (x & 63);
     S.load.assign(NS, 0);
     int32_t low = 0;
+    if (WD == 1) {             // NS <= 64: one word per level
+        uint64_t* L = S.lvl.data();
+        const size_t U = S.order.size();
+        for (size_t k = 0; k < U;) {
+            while (!L[low]) ++low;
+            if ((int64_t)low + 1 >= cap) {                        // grow (never reached)
+                S.lvl.resize((size_t)low + 2, 0);
+                cap = (int64_t)low + 2;
+                L = S.lvl.data();
+            }
+            const int32_t ul0 = S.order[k];
+            if (S.ucnt[ul0] == 1) {
+                // degree 1 from here on (falling degree): the users take the
+                // level's slots in ascending order, each to level low + 1 --
+                // what one user at a time would do
+                uint64_t b = L[low], moved = 0;
+                for (; b && k < U; b &= b - 1) {
+                    const int32_t slot = __builtin_ctzll(b), ul = S.order[k++];
+                    moved |= 1ull << slot;
+                    S.uslot[ul] = slot;
+                    S.load[slot] = low + 1;
+                }
+                L[low] = b;
+                L[low + 1] |= moved;
+                D = std::max(D, low + 1);
+                continue;
+            }
+            const int32_t slot = __builtin_ctzll(L[low]);
+            L[low] &= L[low] - 1;
+            const int32_t nl = low + S.ucnt[ul0];
+            if (nl >= cap) {                                      // grow (never reached)
+                S.lvl.resize((size_t)nl + 1, 0);
+                cap = (int64_t)nl + 1;
+                L = S.lvl.data();
+            }
+            L[nl] |= 1ull << slot;
+            S.uslot[ul0] = slot;
+            S.load[slot] = nl;
+            D = std::max(D, nl);
+            ++k;
+        }
+    } else
     for (int32_t ul : S.order) {
         while (true) {                                            // lowest non-empty level
             bool any = false;
