@@ -225,13 +225,20 @@ colour:
         throw std::length_error("a strata block's grid of D x NS positions reaches 2^31");
     const auto c2 = clk::now();
     // Koenig edge colouring with D colours
-    S.sc.assign((size_t)NS * D, -1);
-    S.ic.assign((size_t)nqi * D, -1);
-    S.ecol.assign(m, -1);
+    S.ecol.resize(m);
     auto set = [&](int32_t e, int32_t c) {
         S.ecol[e] = c;
         S.sc[(size_t)S.es[e] * D + c] = e;
         S.ic[(size_t)S.eq[e] * D + c] = e;
+    };
+    // the (slot, colour) and (item, colour) -> edge tables, for the repairs;
+    // with masks they are built at the first repair, from the colours so far
+    bool tables = false;
+    auto build_tables = [&](int32_t upto) {
+        S.sc.assign((size_t)NS * D, -1);
+        S.ic.assign((size_t)nqi * D, -1);
+        for (int32_t x = 0; x < upto; ++x) set(x, S.ecol[x]);
+        tables = true;
     };
     // used-colour masks per slot and per item (D <= 64): a colour free at both
     // ends is found in O(1), and the alternating-path repair runs only when
@@ -240,6 +247,8 @@ colour:
     if (masks) {
         S.smask.assign(NS, 0);
         S.imask.assign(nqi, 0);
+    } else {
+        build_tables(0);
     }
     for (int32_t e = 0; e < m; ++e) {
         const int32_t s = S.es[e], q = S.eq[e];
@@ -247,11 +256,13 @@ colour:
             const uint64_t both = S.smask[s] | S.imask[q];
             if (~both & (D == 64 ? ~0ull : ((1ull << D) - 1))) {
                 const int32_t c = __builtin_ctzll(~both);
-                set(e, c);
+                if (tables) set(e, c);
+                else S.ecol[e] = c;
                 S.smask[s] |= 1ull << c;
                 S.imask[q] |= 1ull << c;
                 continue;
             }
+            if (!tables) build_tables(e);
         }
         const int32_t* scs = &S.sc[(size_t)s * D];
         const int32_t* ics = &S.ic[(size_t)q * D];
