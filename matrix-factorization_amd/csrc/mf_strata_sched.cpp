@@ -459,14 +459,16 @@ static int plan_build(const int32_t* user_ids, const int32_t* item_ids, int64_t 
     mf::for_buckets(CB, T, [&](int sv) {
         const int64_t lo = soff[sv], hi = soff[sv + 1];
         std::vector<int64_t> cnt((size_t)B + 1, 0);
-        for (int64_t d = lo; d < hi; ++d) ++cnt[ib_of[strip[d].i] + 1];
+        thread_local std::vector<int32_t> wv;     // each row's item range, looked up once
+        wv.resize((size_t)(hi - lo));
+        for (int64_t d = lo; d < hi; ++d) {
+            const int32_t w = ib_of[strip[d].i];
+            wv[(size_t)(d - lo)] = w;
+            ++cnt[w + 1];
+        }
         for (int32_t w = 0; w < B; ++w) cnt[w + 1] += cnt[w];
         for (int32_t w = 0; w < B; ++w) boff[(size_t)sv * B + w] = lo + cnt[w];
-        for (int64_t d = lo; d < hi; ++d) {
-            const Trip t = strip[d];
-            const int64_t o = lo + cnt[ib_of[t.i]]++;
-            b_t[o] = t;
-        }
+        for (int64_t d = lo; d < hi; ++d) b_t[lo + cnt[wv[(size_t)(d - lo)]]++] = strip[d];
     });
     boff[BB] = n;
     strip.reset();
